@@ -1,0 +1,99 @@
+/* md2.h -- C ABI of libmd2hip.so, the MI355X (gfx950) hot path of the Monodepth2.jl train step.
+ *
+ * Every entry point is extern "C", takes plain pointers/sizes (device pointers unless noted),
+ * returns 0 on success or an MD2_E* code, and leaves a message for md2_last_error().
+ * `stream` is a hipStream_t passed as void* (NULL = the legacy default stream).
+ *
+ * Layout: Julia column-major (W,H,C,N) arrays are memory-identical to the C-order [N][C][H][W]
+ * arrays used here, so a Julia ccall shim passes pointers without transposes.
+ * Small matrices (K, invK, R) are ROW-major 3x3 here; the Julia shim passes permutedims(K).
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   md2_loss_*            src/training.jl:21-78  train_loss after the model call (+ Zygote pullback)
+ *   md2_so3_compose_*     src/utils.jl:106-145,185-192  so3_exp_map / hat rrule / composeT
+ *   md2_conv2d_*          Flux Conv + NNlib conv / ∇conv_data / ∇conv_filter (depth/pose decoders,
+ *                         ResNet.jl encoder)
+ *   md2_model_*           src/model.jl:24-70 Model / eval_poses / eval_disparity,
+ *                         src/depth_decoder.jl, src/pose_decoder.jl, ResNet.jl ResidualNetwork
+ *   md2_model_train_*     the gradient(θ) + update!(ADAM) loop of scripts/script.jl:84-86 and
+ *                         src/simple_depth.jl:25-42
+ */
+#ifndef MD2_H
+#define MD2_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MD2_ABI_VERSION 1
+
+#define MD2_OK 0
+#define MD2_EINVAL 1
+#define MD2_EHIP 2
+#define MD2_ENOTSUP 3
+#define MD2_ENOMEM 4
+#define MD2_ESTATE 5
+
+int md2_abi_version(void);
+/* thread-local message of the last failing call (never NULL). */
+const char* md2_last_error(void);
+/* number of visible HIP devices (host call; does not initialise a context). */
+int md2_device_count(int* count);
+
+/* ------------------------------------------------------------------------------------------
+ * Loss tail: src/training.jl:25-77 (given the model's disparities and poses) -- forward value
+ * AND the Zygote pullback in one pass per scale.
+ * ---------------------------------------------------------------------------------------- */
+#define MD2_MAX_SCALES 5
+
+typedef struct md2_loss_cfg {
+  int n;                       /* samples (Params.batch_size)                                */
+  int c;                       /* image channels (1 or 3)                                    */
+  int width, height;           /* Params.target_size                                         */
+  int nscales;                 /* length(TrainCache.scales)                                  */
+  int scale_w[MD2_MAX_SCALES]; /* disparity resolution of each scale                         */
+  int scale_h[MD2_MAX_SCALES];
+  float smooth_weight[MD2_MAX_SCALES]; /* train_loss: disparity_smoothness * scale           */
+  float divisor;               /* train_loss: nscales (training.jl:77); slow_depth: 1         */
+  int smooth_normalize;        /* 1: disparity / (mean + 1e-7) (training.jl:64-65)           */
+  float K[9];                  /* TrainCache.K, row-major                                    */
+  float invK[9];               /* TrainCache.invK, row-major                                 */
+  float min_depth, max_depth;  /* Params                                                      */
+  long long x_sample_stride;   /* elements between samples of x (L*C*H*W for x[N][L][C][H][W]) */
+  long long x_frame_stride;    /* elements between frames (C*H*W)                            */
+  int target, src0, src1;      /* 0-based frame ids (TrainCache.target_id-1, source_ids-1)   */
+  int invert_mask;             /* bit s set: source s < target (training.jl:29)              */
+  int sigmoid_grad;            /* 1: d_disp w.r.t. the sigmoid head pre-activation           */
+} md2_loss_cfg;
+
+size_t md2_loss_workspace_size(const md2_loss_cfg* cfg);
+
+/* Outputs of md2_loss_fwd_bwd (device pointers; NULL = not wanted, except loss). */
+typedef struct md2_loss_out {
+  float* loss;                       /* [1]  train_loss value                                 */
+  float* terms;                      /* [nscales][2] mean warp loss, weighted smooth term     */
+  float* d_disp[MD2_MAX_SCALES];     /* d loss / d disp[s] (or / d pre-sigmoid, cfg)          */
+  float* d_pose;                     /* [2n][6] d loss / d (rvec, tvec)                       */
+  float* vis_loss;                   /* [nscales][n][h][w] per-pixel warp loss (vis_loss)     */
+  signed char* vis_sel;              /* [nscales][n][h][w] argmin source (-1 = automask)      */
+} md2_loss_out;
+
+/* disp[s]: [n][scale_h][scale_w]; pose: [2n][6] = (rvec, tvec) for (source s, sample i) at row
+ * s*n+i; x: frames; automask: [n][h][w] identity-reprojection loss or NULL (Params.automasking).
+ * dloss: upstream gradient of the scalar loss (1 for gradient(θ)). */
+int md2_loss_fwd_bwd(const md2_loss_cfg* cfg, const float* const* disp, const float* pose,
+                     const float* x, const float* automask, float dloss,
+                     const md2_loss_out* out, void* workspace, void* stream);
+
+/* composeT(so3_exp_map(rvec), tvec, invert) for 2n poses -> Rt [2n][12] (R row-major, t). */
+int md2_so3_compose_fwd(const float* pose, int n, int invert_mask, float* Rt, void* stream);
+int md2_so3_compose_bwd(const float* pose, int n, int invert_mask, const float* dRt,
+                        float* d_pose, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MD2_H */

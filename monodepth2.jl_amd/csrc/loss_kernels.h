@@ -1,0 +1,93 @@
+// Loss-tail kernels: see loss_kernels.hip.
+#pragma once
+#include "common.h"
+
+namespace md2 {
+
+constexpr int MAX_SCALES = 5;
+
+// Camera / depth constants of one resolution (TrainCache K, invK; Params min/max depth).
+struct Geom {
+  float K[9];        // row-major
+  float invK[9];     // row-major
+  float min_disp;    // 1 / max_depth
+  float disp_range;  // 1/min_depth - 1/max_depth
+  float wm1, hm1;    // W-1, H-1 (normalize / unnormalize)
+  int W, H;          // full (target) resolution
+};
+
+struct PhotoArgs {
+  const float* disp;      // [N][dh][dw]  (sigmoid output of one scale)
+  int dw, dh;
+  float rx, ry;           // (dw-1)/(W-1), (dh-1)/(H-1)  align_corners upsample ratios
+  const float* x;         // frames
+  long x_sample_stride;   // elements between samples
+  long x_frame_stride;    // elements between frames of a sample
+  int target, src0, src1; // 0-based frame indices
+  const float* Rt;        // [2][N][12]  composed (R row-major, t) per (source, sample)
+  const float* automask;  // [N][H][W] identity-reprojection loss or nullptr
+  float wloss;            // d(total loss) / d(per-pixel warp loss)
+  float* g_disp;          // [N][H][W] out: d loss / d full-res disparity (store)
+  float* partials;        // [blocks][25]: loss sum, dR0(9) dt0(3), dR1(9) dt1(3)
+  float* loss_map;        // [N][H][W] per-pixel warp loss (train_loss vis_loss) or nullptr
+  signed char* sel_map;   // [N][H][W] chosen source (0/1, -1 = automask) or nullptr
+  int N;
+};
+
+struct SmoothArgs {
+  const float* disp;
+  int dw, dh;
+  float rx, ry;
+  const float* img;          // target frame of sample 0 ([C][H][W])
+  long img_sample_stride;
+  const float* mean_partials;  // [N][mean_parts] sums of the upsampled disparity
+  int mean_parts;
+  float ws;                  // d(total)/d(smooth term) = smoothness * scale / nscales * upstream
+  float* g_disp;             // [N][H][W] accumulated
+  float* partials;           // [blocks][2]: smooth loss sum, sum(u * d)
+  int N, W, H;
+};
+
+struct UpAdjArgs {
+  const float* g_full;       // [N][H][W]
+  const float* disp;         // [N][dh][dw] sigmoid output (for the derivative)
+  int dw, dh;
+  float rx, ry;
+  const float* mean_partials;
+  int mean_parts;
+  const float* smooth_partials;  // [N][smooth_parts][2] or nullptr
+  int smooth_parts;
+  float ws;
+  int sigmoid;               // multiply by s(1-s)
+  int accumulate;
+  float* out;                // [N][dh][dw]
+  int N, W, H;
+};
+
+struct FinalizeArgs {
+  const float* photo_partials[MAX_SCALES];
+  long photo_blocks[MAX_SCALES];
+  const float* smooth_partials[MAX_SCALES];
+  long smooth_blocks[MAX_SCALES];
+  float smooth_scale[MAX_SCALES];   // smoothness * scale  (the term's forward weight)
+  float photo_scale;                // 1 / (N*H*W)
+  float* terms;                     // [nscales][2]
+  float divisor;                    // train_loss: nscales; slow_depth: 1
+  int nscales;
+  int N;
+};
+
+int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st);
+long photometric_blocks(int W, int H, int N);
+long smooth_blocks(int W, int H, int N);
+int launch_disp_sum(const float* disp, int dw, int dh, float rx, float ry, int W, int H, int N,
+                    int parts, float* out, hipStream_t st);
+int launch_smooth(const SmoothArgs& a, int C, hipStream_t st);
+int launch_up_adjoint(const UpAdjArgs& a, hipStream_t st);
+int launch_loss_finalize(const FinalizeArgs& a, float* dRt, float* loss, hipStream_t st);
+int launch_so3_fwd(const float* pose, int count, int N, int invert_mask, float* Rt,
+                   hipStream_t st);
+int launch_so3_bwd(const float* pose, int count, int N, int invert_mask, const float* dRt,
+                   float* dpose, int accumulate, hipStream_t st);
+
+}  // namespace md2

@@ -1,0 +1,835 @@
+// Photometric loss tail of the Monodepth2.jl train step, fused forward+backward (gfx950).
+//
+// Reference: src/training.jl:21-78 (train_loss), :1-19 (photometric / prediction / automask),
+// src/utils.jl:17-43 (SSIM), :45-103 (Backproject / Project / normalize), :106-145 (so3 + hat),
+// :163-183 (smooth_loss, disparity_to_depth), :185-192 (composeT).
+//
+// The loss is a pixel MEAN of terminal per-pixel terms, so its gradient w.r.t. every per-pixel
+// term is a known constant: one pass per scale computes the forward value AND the backward
+// (d disparity, d R, d t) with no saved activations.  Per scale and pixel the kernel reads the
+// disparity, the target and two sources (bilinear gathers) and writes one gradient float.
+#include "loss_kernels.h"
+
+namespace md2 {
+
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
+}
+
+// Bilinear align_corners=true upsample of one value (NNlib upsample_bilinear(x; size)),
+// src/training.jl:45.  ratio = (in-1)/(out-1).
+__device__ __forceinline__ float upsample_at(const float* __restrict__ d, int dw, int dh,
+                                             float rx, float ry, int X, int Y) {
+  const float sx = rx * (float)X, sy = ry * (float)Y;
+  int ix0 = (int)sx, iy0 = (int)sy;
+  ix0 = min(ix0, dw - 1);
+  iy0 = min(iy0, dh - 1);
+  const int ix1 = min(ix0 + 1, dw - 1), iy1 = min(iy0 + 1, dh - 1);
+  const float fx = sx - (float)ix0, fy = sy - (float)iy0;
+  const float v00 = d[iy0 * dw + ix0], v01 = d[iy0 * dw + ix1];
+  const float v10 = d[iy1 * dw + ix0], v11 = d[iy1 * dw + ix1];
+  return (1.f - fy) * ((1.f - fx) * v00 + fx * v01) + fy * ((1.f - fx) * v10 + fx * v11);
+}
+
+__device__ __forceinline__ float disp_at(const float* __restrict__ d, int dw, int dh, float rx,
+                                         float ry, int W, int H, int X, int Y) {
+  if (dw == W && dh == H) return d[Y * W + X];
+  return upsample_at(d, dw, dh, rx, ry, X, Y);
+}
+
+struct Proj {
+  float X[3];     // camera point  depth * invK * (w, h, 1)
+  float P[3];     // R X + t
+  float cam[3];   // K P
+  float denom;    // 1 / (cam_z + 1e-7)
+  float ix, iy;   // unnormalised sample coordinate (0-based), before clamping
+};
+
+// src/utils.jl:67-69 (Backproject), :99-103 (Project), :83-85 (normalize), and the NNlib
+// grid_sample unnormalisation ((g + 1)/2)(size - 1) for align_corners = true.
+__device__ __forceinline__ void project_point(const Geom& g, const float* Rt, float depth,
+                                              float ray0, float ray1, float ray2, Proj& p) {
+  p.X[0] = depth * ray0;
+  p.X[1] = depth * ray1;
+  p.X[2] = depth * ray2;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    p.P[i] = Rt[3 * i + 0] * p.X[0] + Rt[3 * i + 1] * p.X[1] + Rt[3 * i + 2] * p.X[2] + Rt[9 + i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    p.cam[i] = g.K[3 * i + 0] * p.P[0] + g.K[3 * i + 1] * p.P[1] + g.K[3 * i + 2] * p.P[2];
+  p.denom = 1.f / (p.cam[2] + 1e-7f);
+  const float u = p.cam[0] * p.denom, v = p.cam[1] * p.denom;
+  const float gx = (((u - 1.f) / g.wm1) - 0.5f) * 2.f;
+  const float gy = (((v - 1.f) / g.hm1) - 0.5f) * 2.f;
+  p.ix = ((gx + 1.f) * 0.5f) * g.wm1;
+  p.iy = ((gy + 1.f) * 0.5f) * g.hm1;
+}
+
+// Border-clamped bilinear sample of C channels (NNlib grid_sample, padding_mode = :border).
+template <int C>
+__device__ __forceinline__ void sample_bilinear(const float* __restrict__ src, long HW, int W,
+                                                int H, float ix, float iy, float (&out)[C]) {
+  const float x = fminf(fmaxf(ix, 0.f), (float)(W - 1));
+  const float y = fminf(fmaxf(iy, 0.f), (float)(H - 1));
+  const int x0 = (int)x, y0 = (int)y;
+  const int x1 = x0 + 1, y1 = y0 + 1;
+  const float fx = x - (float)x0, fy = y - (float)y0;
+  const float w00 = (1.f - fx) * (1.f - fy), w01 = fx * (1.f - fy);
+  const float w10 = (1.f - fx) * fy, w11 = fx * fy;
+  const bool okx = x1 < W, oky = y1 < H;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float* s = src + c * HW;
+    float v = w00 * s[y0 * W + x0];
+    if (okx) v += w01 * s[y0 * W + x1];
+    if (oky) v += w10 * s[y1 * W + x0];
+    if (okx && oky) v += w11 * s[y1 * W + x1];
+    out[c] = v;
+  }
+}
+
+// d(sample)/d(ix, iy) contracted with dout[c] (zero contribution from out-of-range corners),
+// times the border-clip gradient mask (0 when the coordinate was clamped or on the border,
+// PyTorch/NNlib clip_coordinates_set_grad).
+template <int C>
+__device__ __forceinline__ void sample_bilinear_grad(const float* __restrict__ src, long HW,
+                                                     int W, int H, float ix, float iy,
+                                                     const float (&dout)[C], float& dix,
+                                                     float& diy) {
+  const float mx = (ix > 0.f && ix < (float)(W - 1)) ? 1.f : 0.f;
+  const float my = (iy > 0.f && iy < (float)(H - 1)) ? 1.f : 0.f;
+  const float x = fminf(fmaxf(ix, 0.f), (float)(W - 1));
+  const float y = fminf(fmaxf(iy, 0.f), (float)(H - 1));
+  const int x0 = (int)x, y0 = (int)y;
+  const int x1 = x0 + 1, y1 = y0 + 1;
+  const float fx = x - (float)x0, fy = y - (float)y0;
+  const bool okx = x1 < W, oky = y1 < H;
+  float gx = 0.f, gy = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float* s = src + c * HW;
+    const float v00 = s[y0 * W + x0];
+    const float v01 = okx ? s[y0 * W + x1] : 0.f;
+    const float v10 = oky ? s[y1 * W + x0] : 0.f;
+    const float v11 = (okx && oky) ? s[y1 * W + x1] : 0.f;
+    gx += dout[c] * ((v01 - v00) * (1.f - fy) + (v11 - v10) * fy);
+    gy += dout[c] * ((v10 - v00) * (1.f - fx) + (v11 - v01) * fx);
+  }
+  dix = gx * mx;
+  diy = gy * my;
+}
+
+// Back-propagate d(ix, iy) of one source through normalize/Project/Backproject:
+// accumulates dR (9), dt (3) and returns d(depth).
+__device__ __forceinline__ float project_point_grad(const Geom& g, const float* Rt,
+                                                    const Proj& p, float dix, float diy,
+                                                    float ray0, float ray1, float ray2,
+                                                    float* dRt) {
+  // ix = ((gx+1)/2) (W-1),  gx = ((u-1)/(W-1) - 1/2) 2
+  const float du = dix * (g.wm1 * 0.5f) * (2.f / g.wm1);
+  const float dv = diy * (g.hm1 * 0.5f) * (2.f / g.hm1);
+  float dcam[3];
+  dcam[0] = du * p.denom;
+  dcam[1] = dv * p.denom;
+  dcam[2] = -(du * p.cam[0] + dv * p.cam[1]) * p.denom * p.denom;
+  float dP[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) dP[j] = g.K[j] * dcam[0] + g.K[3 + j] * dcam[1] + g.K[6 + j] * dcam[2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dRt[3 * i + j] += dP[i] * p.X[j];
+    dRt[9 + i] += dP[i];
+  }
+  float dX[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) dX[j] = Rt[j] * dP[0] + Rt[3 + j] * dP[1] + Rt[6 + j] * dP[2];
+  return dX[0] * ray0 + dX[1] * ray1 + dX[2] * ray2;
+}
+
+__device__ __forceinline__ void ray_at(const Geom& g, int gx, int gy, float& r0, float& r1,
+                                       float& r2) {
+  const float w = (float)(gx + 1), h = (float)(gy + 1);   // 1-based grid (src/utils.jl:51-55)
+  r0 = g.invK[0] * w + g.invK[1] * h + g.invK[2];
+  r1 = g.invK[3] * w + g.invK[4] * h + g.invK[5];
+  r2 = g.invK[6] * w + g.invK[7] * h + g.invK[8];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused warp + SSIM + L1 + min-over-sources (+ automask) forward and backward, one scale.
+// Tile 32x8 output pixels per 256-thread block; LDS holds warped sources / target on a halo-2
+// region, SSIM adjoint coefficients on a halo-1 region.
+// ---------------------------------------------------------------------------------------------
+constexpr int PT_W = 32, PT_H = 8;
+
+template <int C>
+__global__ __launch_bounds__(256) void photometric_kernel(PhotoArgs a, Geom g) {
+  constexpr int AW = PT_W + 4, AH = PT_H + 4, NA = AW * AH;
+  constexpr int BW = PT_W + 2, BH = PT_H + 2, NB = BW * BH;
+  // per halo-1 pixel p and channel: SSIM partials w.r.t. (mu_x, var_x, cov_xy) of the selected
+  // source, and the window means mu_x(p), mu_y(p) -- the adjoint is evaluated in the centred
+  // form g_m + 2 g_v (x_q - mu_x) + g_c (y_q - mu_y), which avoids the fp32 cancellation of the
+  // literal E[x^2] - E[x]^2 formulation on smooth images.
+  constexpr int NCOEF = 4;   // g_m, g_v, g_c, mu_x
+  __shared__ float s_x[2][C][NA];
+  __shared__ float s_y[C][NA];
+  __shared__ float s_coef[NCOEF * C][NB];
+  __shared__ float s_my[C][NB];
+  __shared__ int s_sel[NB];
+  __shared__ float s_red[4 * 25];
+
+  const int W = g.W, H = g.H;
+  const long HW = (long)W * H;
+  const int n = blockIdx.z;
+  const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
+  const float* xs = a.x + (long)n * a.x_sample_stride;
+  const float* tgt = xs + (long)a.target * a.x_frame_stride;
+  const float* src0 = xs + (long)a.src0 * a.x_frame_stride;
+  const float* src1 = xs + (long)a.src1 * a.x_frame_stride;
+  const float* dsp = a.disp + (long)n * a.dw * a.dh;
+  float Rt0[12], Rt1[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    Rt0[i] = a.Rt[(long)n * 12 + i];
+    Rt1[i] = a.Rt[(long)(a.N + n) * 12 + i];
+  }
+
+  // ---- phase 1: warps + target on the halo-2 region --------------------------------------
+  for (int i = threadIdx.x; i < NA; i += 256) {
+    const int gx = x0 - 2 + (i % AW), gy = y0 - 2 + (i / AW);
+    if (gx < 0 || gx >= W || gy < 0 || gy >= H) continue;
+    const float d = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy);
+    const float depth = 1.f / (d * g.disp_range + g.min_disp);
+    float r0, r1, r2;
+    ray_at(g, gx, gy, r0, r1, r2);
+    Proj p;
+    float v[C];
+    project_point(g, Rt0, depth, r0, r1, r2, p);
+    sample_bilinear<C>(src0, HW, W, H, p.ix, p.iy, v);
+#pragma unroll
+    for (int c = 0; c < C; ++c) s_x[0][c][i] = v[c];
+    project_point(g, Rt1, depth, r0, r1, r2, p);
+    sample_bilinear<C>(src1, HW, W, H, p.ix, p.iy, v);
+#pragma unroll
+    for (int c = 0; c < C; ++c) s_x[1][c][i] = v[c];
+#pragma unroll
+    for (int c = 0; c < C; ++c) s_y[c][i] = tgt[c * HW + (long)gy * W + gx];
+  }
+  __syncthreads();
+
+  // ---- phase 2: SSIM + L1 per source on the halo-1 region, min, adjoint coefficients -------
+  float thread_loss = 0.f;
+  const float kS = a.wloss * 0.85f / (float)C * (1.f / 9.f);
+  const float c1 = 1e-4f, c2 = 9e-4f;
+  const float ninth = 1.f / 9.f;
+  for (int i = threadIdx.x; i < NB; i += 256) {
+    const int bx = i % BW, by = i / BW;
+    const int gx = x0 - 1 + bx, gy = y0 - 1 + by;
+    if (gx < 0 || gx >= W || gy < 0 || gy >= H) continue;
+    int wi[9];
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int ax = reflect_idx(gx + dx, W) - (x0 - 2);
+        const int ay = reflect_idx(gy + dy, H) - (y0 - 2);
+        wi[(dy + 1) * 3 + dx + 1] = ay * AW + ax;
+      }
+    const int ci = (by + 1) * AW + (bx + 1);     // centre in region A
+    float loss_s[2] = {0.f, 0.f};
+    float coef[2][NCOEF * C];
+    float myv[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      // window moments shifted by the centre value (exact algebra, better fp32 conditioning)
+      const float yc = s_y[c][ci];
+      float sy = 0.f, syy = 0.f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const float dv = s_y[c][wi[k]] - yc;
+        sy += dv;
+        syy += dv * dv;
+      }
+      const float eyd = sy * ninth;
+      const float my = yc + eyd, vy = syy * ninth - eyd * eyd;
+      myv[c] = my;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const float xc = s_x[s][c][ci];
+        float sx = 0.f, sxx = 0.f, sxy = 0.f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const float dx = s_x[s][c][wi[k]] - xc;
+          const float dy = s_y[c][wi[k]] - yc;
+          sx += dx;
+          sxx += dx * dx;
+          sxy += dx * dy;
+        }
+        const float exd = sx * ninth;
+        const float mx = xc + exd;
+        const float vx = sxx * ninth - exd * exd, cxy = sxy * ninth - exd * eyd;
+        const float A1 = 2.f * mx * my + c1, A2 = 2.f * cxy + c2;
+        const float B1 = mx * mx + my * my + c1, B2 = vx + vy + c2;
+        const float num = A1 * A2, den = B1 * B2;
+        const float val = (1.f - num / den) * 0.5f;
+        const float sv = fminf(fmaxf(val, 0.f), 1.f);
+        loss_s[s] += 0.85f / (float)C * sv + 0.15f / (float)C * fabsf(yc - xc);
+        const float live = (val >= 0.f && val <= 1.f) ? 1.f : 0.f;
+        const float dn = -0.5f / den * live, dd = 0.5f * num / (den * den) * live;
+        coef[s][NCOEF * c + 0] = kS * (dn * 2.f * my * A2 + dd * 2.f * mx * B2);  // d/d mu_x
+        coef[s][NCOEF * c + 1] = kS * dd * B1;                                    // d/d var_x
+        coef[s][NCOEF * c + 2] = kS * dn * 2.f * A1;                              // d/d cov_xy
+        coef[s][NCOEF * c + 3] = mx;
+      }
+    }
+    // minimum over sources (first argmin), then optional automask (mask first => wins ties)
+    int sel = (loss_s[1] < loss_s[0]) ? 1 : 0;
+    float lmin = sel ? loss_s[1] : loss_s[0];
+    if (a.automask) {
+      const float am = a.automask[((long)n * H + gy) * W + gx];
+      if (!(lmin < am)) {
+        sel = -1;
+        lmin = am;
+      }
+    }
+    s_sel[i] = sel;
+#pragma unroll
+    for (int k = 0; k < NCOEF * C; ++k) s_coef[k][i] = sel == 1 ? coef[1][k] : coef[0][k];
+#pragma unroll
+    for (int c = 0; c < C; ++c) s_my[c][i] = myv[c];
+    if (bx >= 1 && bx <= PT_W && by >= 1 && by <= PT_H) {
+      thread_loss += lmin;
+      const long q = ((long)n * H + gy) * W + gx;
+      if (a.loss_map) a.loss_map[q] = lmin;
+      if (a.sel_map) a.sel_map[q] = (signed char)sel;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 3: adjoint of the 3x3 reflect windows at q, then the geometry backward --------
+  float acc[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) acc[k] = 0.f;
+  acc[0] = thread_loss;
+  const int tx = threadIdx.x % PT_W, ty = threadIdx.x / PT_W;
+  const int gx = x0 + tx, gy = y0 + ty;
+  if (gx < W && gy < H) {
+    const int ai = (ty + 2) * AW + (tx + 2);
+    float xq[2][C], yq[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      xq[0][c] = s_x[0][c][ai];
+      xq[1][c] = s_x[1][c][ai];
+      yq[c] = s_y[c][ai];
+    }
+    float dxs[2][C];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < C; ++c) dxs[s][c] = 0.f;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int py = gy + dy;
+      if (py < 0 || py >= H) continue;
+      const float wy = 1.f + ((gy == 1 && py == 0) ? 1.f : 0.f) + ((gy == H - 2 && py == H - 1) ? 1.f : 0.f);
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int px = gx + dx;
+        if (px < 0 || px >= W) continue;
+        const float wx = 1.f + ((gx == 1 && px == 0) ? 1.f : 0.f) + ((gx == W - 2 && px == W - 1) ? 1.f : 0.f);
+        const int bi = (py - (y0 - 1)) * BW + (px - (x0 - 1));
+        const int sel = s_sel[bi];
+        if (sel < 0) continue;
+        const float w = wx * wy;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const float xv = sel ? xq[1][c] : xq[0][c];
+          const float t = s_coef[NCOEF * c + 0][bi] +
+                          2.f * s_coef[NCOEF * c + 1][bi] * (xv - s_coef[NCOEF * c + 3][bi]) +
+                          s_coef[NCOEF * c + 2][bi] * (yq[c] - s_my[c][bi]);
+          if (sel)
+            dxs[1][c] += w * t;
+          else
+            dxs[0][c] += w * t;
+        }
+      }
+    }
+    const int bq = (ty + 1) * BW + (tx + 1);
+    const int selq = s_sel[bq];
+    const float kL = a.wloss * 0.15f / (float)C;
+    bool any[2] = {false, false};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        if (selq == s) {
+          const float df = xq[s][c] - yq[c];   // d|y - x|/dx = sign(x - y), abs'(0) = 0
+          dxs[s][c] += kL * (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f));
+        }
+        any[s] = any[s] || (dxs[s][c] != 0.f);
+      }
+    }
+    const float dval = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy);
+    const float depth = 1.f / (dval * g.disp_range + g.min_disp);
+    float r0, r1, r2;
+    ray_at(g, gx, gy, r0, r1, r2);
+    float ddepth = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (!any[s]) continue;
+      const float* Rt = s ? Rt1 : Rt0;
+      Proj p;
+      project_point(g, Rt, depth, r0, r1, r2, p);
+      float dix, diy;
+      sample_bilinear_grad<C>(s ? src1 : src0, HW, W, H, p.ix, p.iy, dxs[s], dix, diy);
+      ddepth += project_point_grad(g, Rt, p, dix, diy, r0, r1, r2, &acc[1 + 12 * s]);
+    }
+    // depth = 1/(disp*range + min_disp)  =>  d depth/d disp = -range * depth^2
+    a.g_disp[((long)n * H + gy) * W + gx] = -ddepth * g.disp_range * depth * depth;
+  }
+  block_sum256<25>(acc, s_red);
+  if (threadIdx.x == 0) {
+    const long blk = ((long)n * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+#pragma unroll
+    for (int k = 0; k < 25; ++k) a.partials[blk * 25 + k] = acc[k];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-image mean of the (upsampled) disparity -- src/training.jl:64-65
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void disp_sum_kernel(const float* __restrict__ disp, int dw,
+                                                       int dh, float rx, float ry, int W, int H,
+                                                       int parts, float* __restrict__ out) {
+  __shared__ float red[4];
+  const int n = blockIdx.y;
+  const long P = (long)W * H;
+  const float* d = disp + (long)n * dw * dh;
+  float s = 0.f;
+  for (long q = (long)blockIdx.x * 256 + threadIdx.x; q < P; q += (long)parts * 256) {
+    const int X = (int)(q % W), Y = (int)(q / W);
+    s += disp_at(d, dw, dh, rx, ry, W, H, X, Y);
+  }
+  float v[1] = {s};
+  block_sum256<1>(v, red);
+  if (threadIdx.x == 0) out[n * parts + blockIdx.x] = v[0];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Edge-aware smoothness on the mean-normalised full-res disparity (src/utils.jl:163-177,
+// src/training.jl:64-67), forward + the local part of the backward.
+// ---------------------------------------------------------------------------------------------
+constexpr int SM_W = 64, SM_H = 4;
+
+template <int C>
+__global__ __launch_bounds__(256) void smooth_kernel(SmoothArgs a) {
+  constexpr int EW = SM_W + 1, EH = SM_H + 1, NE = EW * EH;
+  __shared__ float s_ex[NE], s_ey[NE];
+  __shared__ float s_red[4 * 3];
+  const int W = a.W, H = a.H;
+  const long HW = (long)W * H;
+  const int n = blockIdx.z;
+  const int x0 = blockIdx.x * SM_W, y0 = blockIdx.y * SM_H;
+  const float* dsp = a.disp + (long)n * a.dw * a.dh;
+  const float* img = a.img + (long)n * a.img_sample_stride;
+  float inv = 1.f;                          // slow_depth: no mean normalisation
+  if (a.mean_partials) {
+    float m = 0.f;
+    for (int k = 0; k < a.mean_parts; ++k) m += a.mean_partials[n * a.mean_parts + k];
+    m = m / (float)HW;
+    inv = 1.f / (m + 1e-7f);
+  }
+  const float cx = 1.f / ((float)a.N * (float)H * (float)(W - 1));
+  const float cy = 1.f / ((float)a.N * (float)(H - 1) * (float)W);
+  float lx = 0.f, ly = 0.f;
+  for (int i = threadIdx.x; i < NE; i += 256) {
+    const int ex = i % EW, ey = i / EW;
+    const int gx = x0 - 1 + ex, gy = y0 - 1 + ey;
+    float vx = 0.f, vy = 0.f;
+    if (gx >= 0 && gx < W && gy >= 0 && gy < H) {
+      // differences are formed on the raw disparity and scaled afterwards: (d_q - d_r) * inv is
+      // sign-exact (no FMA-contraction residue where d_q == d_r, abs'(0) = 0)
+      const float dq = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy);
+      const bool own = ex >= 1 && ey >= 1;
+      if (gx + 1 < W) {
+        const float dr = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx + 1, gy);
+        float gi = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          gi += fabsf(img[c * HW + (long)gy * W + gx] - img[c * HW + (long)gy * W + gx + 1]);
+        const float e = expf(-gi / (float)C) * cx;
+        const float df = (dq - dr) * inv;
+        vx = e * (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f));
+        if (own) lx += fabsf(df) * e;
+      }
+      if (gy + 1 < H) {
+        const float dd = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy + 1);
+        float gi = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          gi += fabsf(img[c * HW + (long)gy * W + gx] - img[c * HW + (long)(gy + 1) * W + gx]);
+        const float e = expf(-gi / (float)C) * cy;
+        const float df = (dq - dd) * inv;
+        vy = e * (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f));
+        if (own) ly += fabsf(df) * e;
+      }
+    }
+    s_ex[i] = vx;
+    s_ey[i] = vy;
+  }
+  __syncthreads();
+  float tsum = 0.f;
+  for (int i = threadIdx.x; i < SM_W * SM_H; i += 256) {
+    const int tx = i % SM_W, ty = i / SM_W;
+    const int gx = x0 + tx, gy = y0 + ty;
+    if (gx >= W || gy >= H) continue;
+    const int e = (ty + 1) * EW + (tx + 1);
+    const float u = s_ex[e] - s_ex[e - 1] + s_ey[e] - s_ey[e - EW];
+    const long q = ((long)n * H + gy) * W + gx;
+    a.g_disp[q] += a.ws * u * inv;
+    tsum += u * disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy);
+  }
+  float v[3] = {lx + ly, tsum, 0.f};
+  block_sum256<3>(v, s_red);
+  if (threadIdx.x == 0) {
+    const long blk = ((long)n * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    a.partials[blk * 2 + 0] = v[0];
+    a.partials[blk * 2 + 1] = v[1];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Adjoint of the align_corners bilinear upsample (+ the mean-normalisation constant and the
+// optional sigmoid derivative of the disparity head), one low-res pixel per thread.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void up_range(int j, int in, int out, float r, int& lo, int& hi) {
+  if (in == 1) {
+    lo = 0;
+    hi = out - 1;
+    return;
+  }
+  lo = max(0, (int)floorf((float)(j - 1) / r) - 1);
+  hi = min(out - 1, (int)ceilf((float)(j + 1) / r) + 1);
+}
+
+__device__ __forceinline__ float up_weight(int X, int j, int in, float r) {
+  const float sx = r * (float)X;
+  int i0 = (int)sx;
+  i0 = min(i0, in - 1);
+  const int i1 = min(i0 + 1, in - 1);
+  const float f = sx - (float)i0;
+  return (i0 == j ? 1.f - f : 0.f) + (i1 == j ? f : 0.f);
+}
+
+__global__ __launch_bounds__(256) void up_adjoint_kernel(UpAdjArgs a) {
+  const int W = a.W, H = a.H;
+  const long total = (long)a.N * a.dw * a.dh;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int j = (int)(idx % a.dw);
+  const int i = (int)((idx / a.dw) % a.dh);
+  const int n = (int)(idx / ((long)a.dw * a.dh));
+  float cn = 0.f;
+  if (a.smooth_partials) {
+    float m = 0.f, T = 0.f;
+    for (int k = 0; k < a.mean_parts; ++k) m += a.mean_partials[n * a.mean_parts + k];
+    for (int k = 0; k < a.smooth_parts; ++k) T += a.smooth_partials[((long)n * a.smooth_parts + k) * 2 + 1];
+    m = m / ((float)W * (float)H);
+    const float mi = 1.f / (m + 1e-7f);
+    cn = -a.ws * T * mi * mi / ((float)W * (float)H);
+  }
+  const float* g = a.g_full + (long)n * W * H;
+  float acc = 0.f;
+  if (a.dw == W && a.dh == H) {
+    acc = g[(long)i * W + j] + cn;
+  } else {
+    int xlo, xhi, ylo, yhi;
+    up_range(j, a.dw, W, a.rx, xlo, xhi);
+    up_range(i, a.dh, H, a.ry, ylo, yhi);
+    float wxs = 0.f;
+    for (int X = xlo; X <= xhi; ++X) wxs += up_weight(X, j, a.dw, a.rx);
+    float wys = 0.f;
+    for (int Y = ylo; Y <= yhi; ++Y) {
+      const float wy = up_weight(Y, i, a.dh, a.ry);
+      wys += wy;
+      if (wy == 0.f) continue;
+      float row = 0.f;
+      for (int X = xlo; X <= xhi; ++X) {
+        const float wx = up_weight(X, j, a.dw, a.rx);
+        if (wx != 0.f) row += wx * g[(long)Y * W + X];
+      }
+      acc += wy * row;
+    }
+    acc += cn * wxs * wys;
+  }
+  if (a.sigmoid) {
+    const float s = a.disp[idx];
+    acc *= s * (1.f - s);
+  }
+  if (a.accumulate)
+    a.out[idx] += acc;
+  else
+    a.out[idx] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Final deterministic reductions: loss scalar and per-(source, sample) dR, dt.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void loss_finalize_kernel(FinalizeArgs a) {
+  __shared__ float red[4 * 2];
+  // one block per scale: sum photometric (col 0 of 25) and smooth (col 0 of 2) partials
+  const int s = blockIdx.x;
+  float v[2] = {0.f, 0.f};
+  for (long k = threadIdx.x; k < a.photo_blocks[s]; k += 256) v[0] += a.photo_partials[s][k * 25];
+  for (long k = threadIdx.x; k < a.smooth_blocks[s]; k += 256) v[1] += a.smooth_partials[s][k * 2];
+  block_sum256<2>(v, red);
+  if (threadIdx.x == 0) {
+    a.terms[2 * s + 0] = v[0] * a.photo_scale;         // mean(warp_loss)
+    a.terms[2 * s + 1] = v[1] * a.smooth_scale[s];      // smooth * 1e-3 * scale
+  }
+}
+
+__global__ void loss_total_kernel(const float* terms, int nscales, float divisor, float* loss) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    float l = 0.f;
+    for (int s = 0; s < nscales; ++s) l += terms[2 * s] + terms[2 * s + 1];
+    loss[0] = l / divisor;
+  }
+}
+
+// grid: (2*N) blocks; sums the 24 pose values of every block of image n over all scales.
+__global__ __launch_bounds__(256) void pose_grad_reduce_kernel(FinalizeArgs a, float* dRt) {
+  __shared__ float red[4 * 12];
+  const int q = blockIdx.x;            // q = s*N + n
+  const int s = q / a.N, n = q % a.N;
+  float v[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) v[k] = 0.f;
+  for (int sc = 0; sc < a.nscales; ++sc) {
+    const long per = a.photo_blocks[sc] / a.N;
+    const float* p = a.photo_partials[sc] + (long)n * per * 25;
+    for (long b = threadIdx.x; b < per; b += 256) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) v[k] += p[b * 25 + 1 + 12 * s + k];
+    }
+  }
+  block_sum256<12>(v, red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) dRt[(long)q * 12 + k] = v[k];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// so3_exp_map + composeT forward / backward (src/utils.jl:106-145, 185-192).
+// pose [2N][6] = (rvec, tvec) per (source, sample); invert flag per source.
+// ---------------------------------------------------------------------------------------------
+struct So3Tmp {
+  float S[9], S2[9], f1, f2, th, thi;
+};
+
+__device__ __forceinline__ void so3_core(const float* r, So3Tmp& t) {
+  t.S[0] = 0.f;   t.S[1] = -r[2]; t.S[2] = r[1];
+  t.S[3] = r[2];  t.S[4] = 0.f;   t.S[5] = -r[0];
+  t.S[6] = -r[1]; t.S[7] = r[0];  t.S[8] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      t.S2[3 * i + j] = t.S[3 * i] * t.S[j] + t.S[3 * i + 1] * t.S[3 + j] + t.S[3 * i + 2] * t.S[6 + j];
+  t.th = sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+  t.thi = 1.f / fmaxf(t.th, 1e-4f);
+  t.f1 = t.thi * sinf(t.th);
+  t.f2 = t.thi * t.thi * (1.f - cosf(t.th));
+}
+
+__global__ void so3_fwd_kernel(const float* __restrict__ pose, int count, int N, int invert_mask,
+                               float* __restrict__ Rt) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= count) return;
+  const int s = q / N;
+  const float* r = pose + q * 6;
+  So3Tmp t;
+  so3_core(r, t);
+  float R[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = t.f1 * t.S[k] + t.f2 * t.S2[k] + ((k % 4) == 0 ? 1.f : 0.f);
+  const float tv[3] = {pose[q * 6 + 3], pose[q * 6 + 4], pose[q * 6 + 5]};
+  float* o = Rt + q * 12;
+  if ((invert_mask >> s) & 1) {
+    // R' = R^T, t' = R' (-t)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) o[3 * i + j] = R[3 * j + i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[9 + i] = -(o[3 * i] * tv[0] + o[3 * i + 1] * tv[1] + o[3 * i + 2] * tv[2]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) o[k] = R[k];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[9 + i] = tv[i];
+  }
+}
+
+__global__ void so3_bwd_kernel(const float* __restrict__ pose, int count, int N, int invert_mask,
+                               const float* __restrict__ dRt, float* __restrict__ dpose,
+                               int accumulate) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= count) return;
+  const int s = q / N;
+  const float* r = pose + q * 6;
+  So3Tmp t;
+  so3_core(r, t);
+  float R[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = t.f1 * t.S[k] + t.f2 * t.S2[k] + ((k % 4) == 0 ? 1.f : 0.f);
+  const float tv[3] = {pose[q * 6 + 3], pose[q * 6 + 4], pose[q * 6 + 5]};
+  const float* g = dRt + q * 12;
+  float dR[9], dt[3];
+  if ((invert_mask >> s) & 1) {
+    // R' = R^T; t' = -R' t.  dR'_ij += -dt'_i t_j ;  dt = -R'^T dt' = -R dt'
+    float dRp[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dRp[3 * i + j] = g[3 * i + j] - g[9 + i] * tv[j];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dR[3 * i + j] = dRp[3 * j + i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dt[i] = -(R[3 * i] * g[9] + R[3 * i + 1] * g[10] + R[3 * i + 2] * g[11]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) dR[k] = g[k];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dt[i] = g[9 + i];
+  }
+  // R = f1 S + f2 S^2 + I
+  float dS[9];
+  float df1 = 0.f, df2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    df1 += dR[k] * t.S[k];
+    df2 += dR[k] * t.S2[k];
+  }
+  // d/dS <dR, S^2> = dR S^T + S^T dR
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        a1 += dR[3 * i + k] * t.S[3 * j + k];
+        a2 += t.S[3 * k + i] * dR[3 * k + j];
+      }
+      dS[3 * i + j] = t.f1 * dR[3 * i + j] + t.f2 * (a1 + a2);
+    }
+  // f1 = thi sin(th), f2 = thi^2 (1 - cos th), thi = 1/max(th, 1e-4)
+  const float dthi = (t.th > 1e-4f) ? -1.f / (t.th * t.th) : 0.f;
+  const float dth = df1 * (dthi * sinf(t.th) + t.thi * cosf(t.th)) +
+                    df2 * (2.f * t.thi * dthi * (1.f - cosf(t.th)) + t.thi * t.thi * sinf(t.th));
+  float dr[3];
+  dr[0] = dS[7] - dS[5];            // hat rrule, src/utils.jl:139-141
+  dr[1] = dS[2] - dS[6];
+  dr[2] = dS[3] - dS[1];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) dr[k] += dth * r[k] / t.th;   // d sqrt(sum r^2)
+  float* o = dpose + q * 6;
+  if (accumulate) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      o[k] += dr[k];
+      o[3 + k] += dt[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      o[k] = dr[k];
+      o[3 + k] = dt[k];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------------------------
+int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st) {
+  dim3 grid(cdiv(g.W, PT_W), cdiv(g.H, PT_H), a.N);
+  if (C == 3)
+    hipLaunchKernelGGL(photometric_kernel<3>, grid, dim3(256), 0, st, a, g);
+  else if (C == 1)
+    hipLaunchKernelGGL(photometric_kernel<1>, grid, dim3(256), 0, st, a, g);
+  else {
+    set_error("photometric: channels must be 1 or 3");
+    return MD2_ENOTSUP;
+  }
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+long photometric_blocks(int W, int H, int N) { return (long)cdiv(W, PT_W) * cdiv(H, PT_H) * N; }
+long smooth_blocks(int W, int H, int N) { return (long)cdiv(W, SM_W) * cdiv(H, SM_H) * N; }
+
+int launch_disp_sum(const float* disp, int dw, int dh, float rx, float ry, int W, int H, int N,
+                    int parts, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(disp_sum_kernel, dim3(parts, N), dim3(256), 0, st, disp, dw, dh, rx, ry, W,
+                     H, parts, out);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int launch_smooth(const SmoothArgs& a, int C, hipStream_t st) {
+  dim3 grid(cdiv(a.W, SM_W), cdiv(a.H, SM_H), a.N);
+  if (C == 3)
+    hipLaunchKernelGGL(smooth_kernel<3>, grid, dim3(256), 0, st, a);
+  else if (C == 1)
+    hipLaunchKernelGGL(smooth_kernel<1>, grid, dim3(256), 0, st, a);
+  else {
+    set_error("smooth: channels must be 1 or 3");
+    return MD2_ENOTSUP;
+  }
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int launch_up_adjoint(const UpAdjArgs& a, hipStream_t st) {
+  const long total = (long)a.N * a.dw * a.dh;
+  hipLaunchKernelGGL(up_adjoint_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int launch_loss_finalize(const FinalizeArgs& a, float* dRt, float* loss, hipStream_t st) {
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(a.nscales), dim3(256), 0, st, a);
+  MD2_LAUNCH_CHECK();
+  hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(64), 0, st, a.terms, a.nscales, a.divisor,
+                     loss);
+  MD2_LAUNCH_CHECK();
+  if (dRt) {
+    hipLaunchKernelGGL(pose_grad_reduce_kernel, dim3(2 * a.N), dim3(256), 0, st, a, dRt);
+    MD2_LAUNCH_CHECK();
+  }
+  return MD2_OK;
+}
+
+int launch_so3_fwd(const float* pose, int count, int N, int invert_mask, float* Rt,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(so3_fwd_kernel, dim3(cdiv(count, 64)), dim3(64), 0, st, pose, count, N,
+                     invert_mask, Rt);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int launch_so3_bwd(const float* pose, int count, int N, int invert_mask, const float* dRt,
+                   float* dpose, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(so3_bwd_kernel, dim3(cdiv(count, 64)), dim3(64), 0, st, pose, count, N,
+                     invert_mask, dRt, dpose, accumulate);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+}  // namespace md2

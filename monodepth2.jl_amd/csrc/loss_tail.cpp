@@ -1,0 +1,163 @@
+// Loss-tail orchestration (src/training.jl:21-78 after the model call).
+#include "loss_tail.h"
+
+#include <cstring>
+
+namespace md2 {
+
+namespace {
+inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+struct TailLayout {
+  size_t Rt, dRt, g_full, mean, photo[MAX_SCALES], smooth[MAX_SCALES], terms, total;
+};
+
+TailLayout layout(const LossTailCfg& c) {
+  TailLayout L{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += align256(bytes);
+    return o;
+  };
+  L.Rt = take(sizeof(float) * 2 * c.N * 12);
+  L.dRt = take(sizeof(float) * 2 * c.N * 12);
+  L.g_full = take(sizeof(float) * (size_t)c.N * c.W * c.H);
+  L.mean = take(sizeof(float) * (size_t)c.nscales * c.N * MEAN_PARTS);
+  for (int s = 0; s < c.nscales; ++s) {
+    L.photo[s] = take(sizeof(float) * 25 * photometric_blocks(c.W, c.H, c.N));
+    L.smooth[s] = take(sizeof(float) * 2 * smooth_blocks(c.W, c.H, c.N));
+  }
+  L.terms = take(sizeof(float) * 2 * MAX_SCALES);
+  L.total = off;
+  return L;
+}
+
+inline float ratio(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
+}  // namespace
+
+size_t loss_tail_workspace_bytes(const LossTailCfg& c) { return layout(c).total; }
+
+int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* pose,
+                  const float* x, const float* automask, float dloss, const LossTailOut& o,
+                  void* workspace, hipStream_t st) {
+  float* loss = o.loss;
+  float* terms = o.terms;
+  const float* const* d_disp = o.d_disp;
+  float* d_pose = o.d_pose;
+  MD2_CHECK_ARG(c.N > 0 && c.W > 2 && c.H > 2, "loss tail dims");
+  MD2_CHECK_ARG(c.nscales >= 1 && c.nscales <= MAX_SCALES, "nscales");
+  MD2_CHECK_ARG(c.C == 1 || c.C == 3, "channels must be 1 or 3");
+  MD2_CHECK_ARG(workspace != nullptr && disp != nullptr && pose != nullptr && x != nullptr,
+                "null pointer");
+  const TailLayout L = layout(c);
+  char* ws = (char*)workspace;
+  float* Rt = (float*)(ws + L.Rt);
+  float* dRt = (float*)(ws + L.dRt);
+  float* g_full = (float*)(ws + L.g_full);
+  float* mean = (float*)(ws + L.mean);
+  float* tterms = terms ? terms : (float*)(ws + L.terms);
+
+  Geom g;
+  std::memcpy(g.K, c.K, sizeof(g.K));
+  std::memcpy(g.invK, c.invK, sizeof(g.invK));
+  g.min_disp = (float)(1.0 / c.max_depth);
+  g.disp_range = (float)(1.0 / c.min_depth - 1.0 / c.max_depth);
+  g.W = c.W;
+  g.H = c.H;
+  g.wm1 = (float)(c.W - 1);
+  g.hm1 = (float)(c.H - 1);
+
+  MD2_TRY(launch_so3_fwd(pose, 2 * c.N, c.N, c.invert_mask, Rt, st));
+
+  const float up = dloss / c.divisor;
+  const long photo_blk = photometric_blocks(c.W, c.H, c.N);
+  const long smooth_blk = smooth_blocks(c.W, c.H, c.N);
+  FinalizeArgs fa{};
+  fa.nscales = c.nscales;
+  fa.N = c.N;
+  fa.photo_scale = 1.f / ((float)c.N * c.W * c.H);
+  fa.terms = tterms;
+  fa.divisor = c.divisor;
+
+  for (int s = 0; s < c.nscales; ++s) {
+    MD2_CHECK_ARG(c.dw[s] >= 1 && c.dh[s] >= 1 && c.dw[s] <= c.W && c.dh[s] <= c.H, "scale dims");
+    const float rx = ratio(c.dw[s], c.W), ry = ratio(c.dh[s], c.H);
+    float* mp = mean + (size_t)s * c.N * MEAN_PARTS;
+    float* pp = (float*)(ws + L.photo[s]);
+    float* sp = (float*)(ws + L.smooth[s]);
+    MD2_TRY(launch_disp_sum(disp[s], c.dw[s], c.dh[s], rx, ry, c.W, c.H, c.N, MEAN_PARTS, mp, st));
+
+    PhotoArgs pa{};
+    pa.disp = disp[s];
+    pa.dw = c.dw[s];
+    pa.dh = c.dh[s];
+    pa.rx = rx;
+    pa.ry = ry;
+    pa.x = x;
+    pa.x_sample_stride = c.x_sample_stride;
+    pa.x_frame_stride = c.x_frame_stride;
+    pa.target = c.target;
+    pa.src0 = c.src0;
+    pa.src1 = c.src1;
+    pa.Rt = Rt;
+    pa.automask = automask;
+    pa.wloss = up / ((float)c.N * c.W * c.H);
+    pa.g_disp = g_full;
+    pa.partials = pp;
+    const size_t plane = (size_t)c.N * c.W * c.H;
+    pa.loss_map = o.vis_loss ? o.vis_loss + s * plane : nullptr;
+    pa.sel_map = o.vis_sel ? o.vis_sel + s * plane : nullptr;
+    pa.N = c.N;
+    MD2_TRY(launch_photometric(pa, g, c.C, st));
+
+    SmoothArgs sa{};
+    sa.disp = disp[s];
+    sa.dw = c.dw[s];
+    sa.dh = c.dh[s];
+    sa.rx = rx;
+    sa.ry = ry;
+    sa.img = x + (long)c.target * c.x_frame_stride;
+    sa.img_sample_stride = c.x_sample_stride;
+    sa.mean_partials = c.smooth_normalize ? mp : nullptr;
+    sa.mean_parts = c.smooth_normalize ? MEAN_PARTS : 0;
+    sa.ws = up * c.smooth_w[s];
+    sa.g_disp = g_full;
+    sa.partials = sp;
+    sa.N = c.N;
+    sa.W = c.W;
+    sa.H = c.H;
+    MD2_TRY(launch_smooth(sa, c.C, st));
+
+    UpAdjArgs ua{};
+    ua.g_full = g_full;
+    ua.disp = disp[s];
+    ua.dw = c.dw[s];
+    ua.dh = c.dh[s];
+    ua.rx = rx;
+    ua.ry = ry;
+    ua.mean_partials = mp;
+    ua.mean_parts = MEAN_PARTS;
+    ua.smooth_partials = c.smooth_normalize ? sp : nullptr;
+    ua.smooth_parts = (int)(smooth_blk / c.N);
+    ua.ws = sa.ws;
+    ua.sigmoid = c.sigmoid_grad;
+    ua.accumulate = 0;
+    ua.out = (float*)d_disp[s];
+    ua.N = c.N;
+    ua.W = c.W;
+    ua.H = c.H;
+    if (d_disp[s]) MD2_TRY(launch_up_adjoint(ua, st));
+
+    fa.photo_partials[s] = pp;
+    fa.photo_blocks[s] = photo_blk;
+    fa.smooth_partials[s] = sp;
+    fa.smooth_blocks[s] = smooth_blk;
+    fa.smooth_scale[s] = c.smooth_w[s];
+  }
+  MD2_TRY(launch_loss_finalize(fa, d_pose ? dRt : nullptr, loss, st));
+  if (d_pose) MD2_TRY(launch_so3_bwd(pose, 2 * c.N, c.N, c.invert_mask, dRt, d_pose, 0, st));
+  return MD2_OK;
+}
+
+}  // namespace md2

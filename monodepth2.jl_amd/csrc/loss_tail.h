@@ -1,0 +1,42 @@
+// Host orchestration of the loss tail: composeT -> per scale {mean, warp+SSIM, smoothness,
+// upsample adjoint} -> deterministic reductions -> composeT/so3 backward.
+#pragma once
+#include "loss_kernels.h"
+
+namespace md2 {
+
+struct LossTailCfg {
+  int N, C, W, H;             // samples, channels, target resolution
+  int nscales;
+  int dw[MAX_SCALES], dh[MAX_SCALES];
+  float smooth_w[MAX_SCALES]; // forward weight of the smooth term (train_loss: smoothness*scale)
+  float divisor;              // train_loss: nscales (src/training.jl:77); slow_depth: 1
+  int smooth_normalize;       // divide the disparity by its per-image mean (training.jl:64-65)
+  float K[9], invK[9];
+  float min_depth, max_depth;
+  long x_sample_stride, x_frame_stride;
+  int target, src0, src1;     // 0-based frame indices
+  int invert_mask;            // bit s: source s uses the inverse transform (src < target)
+  int sigmoid_grad;           // 1: d_disp is w.r.t. the head pre-activation (s(1-s) fused)
+};
+
+constexpr int MEAN_PARTS = 64;
+
+size_t loss_tail_workspace_bytes(const LossTailCfg& c);
+
+struct LossTailOut {
+  float* loss;
+  float* terms;
+  float* d_disp[MAX_SCALES];
+  float* d_pose;
+  float* vis_loss;
+  signed char* vis_sel;
+};
+
+// disp[s]: [N][dh][dw] sigmoid outputs; pose: [2N][6] (rvec, tvec) per (source, sample);
+// x: frames; automask: [N][H][W] or nullptr.  dloss: upstream scalar gradient.
+int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* pose,
+                  const float* x, const float* automask, float dloss, const LossTailOut& o,
+                  void* workspace, hipStream_t st);
+
+}  // namespace md2

@@ -1,0 +1,112 @@
+"""ctypes binding of libmd2hip.so (include/md2.h).
+
+The product path has NO fallback: if the HIP library is missing or fails to load, every call
+raises.  Tensors cross the boundary as raw device pointers (``tensor.data_ptr()``)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MD2HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmd2hip.so"))
+
+MAX_SCALES = 5
+
+
+class LossCfg(C.Structure):
+    """``md2_loss_cfg``."""
+    _fields_ = [
+        ("n", C.c_int), ("c", C.c_int), ("width", C.c_int), ("height", C.c_int),
+        ("nscales", C.c_int),
+        ("scale_w", C.c_int * MAX_SCALES), ("scale_h", C.c_int * MAX_SCALES),
+        ("smooth_weight", C.c_float * MAX_SCALES),
+        ("divisor", C.c_float), ("smooth_normalize", C.c_int),
+        ("K", C.c_float * 9), ("invK", C.c_float * 9),
+        ("min_depth", C.c_float), ("max_depth", C.c_float),
+        ("x_sample_stride", C.c_longlong), ("x_frame_stride", C.c_longlong),
+        ("target", C.c_int), ("src0", C.c_int), ("src1", C.c_int),
+        ("invert_mask", C.c_int), ("sigmoid_grad", C.c_int),
+    ]
+
+
+class LossOut(C.Structure):
+    """``md2_loss_out``."""
+    _fields_ = [
+        ("loss", C.c_void_p), ("terms", C.c_void_p),
+        ("d_disp", C.c_void_p * MAX_SCALES), ("d_pose", C.c_void_p),
+        ("vis_loss", C.c_void_p), ("vis_sel", C.c_void_p),
+    ]
+
+
+_lib = None
+_load_error = None
+
+P = C.c_void_p
+FP = C.POINTER(C.c_void_p)
+
+_SIGS = {
+    "md2_abi_version": (C.c_int, []),
+    "md2_last_error": (C.c_char_p, []),
+    "md2_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "md2_loss_workspace_size": (C.c_size_t, [C.POINTER(LossCfg)]),
+    "md2_loss_fwd_bwd": (C.c_int, [C.POINTER(LossCfg), FP, P, P, P, C.c_float, C.POINTER(LossOut), P, P]),
+    "md2_so3_compose_fwd": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "md2_so3_compose_bwd": (C.c_int, [P, C.c_int, C.c_int, P, P, P]),
+}
+
+
+def lib():
+    """Load libmd2hip.so once (raises if it is missing: there is no CPU fallback)."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libmd2hip.so not found at {LIB_PATH}: run `make -C monodepth2.jl_amd/csrc` "
+                           "(or __graft_entry__.build()); the HIP path has no fallback")
+    # torch must be imported first so that its HIP runtime is the one in the process
+    import torch  # noqa: F401
+    l = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(l, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = l
+    return l
+
+
+def declare(name, restype, argtypes):
+    """Register the signature of an additional exported symbol."""
+    _SIGS[name] = (restype, argtypes)
+    if _lib is not None:
+        f = getattr(_lib, name)
+        f.restype = restype
+        f.argtypes = argtypes
+
+
+class MD2Error(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().md2_last_error().decode(errors="replace")
+        raise MD2Error(f"{what} failed (code {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def ptr_array(ts, n=MAX_SCALES):
+    arr = (C.c_void_p * n)()
+    for i, t in enumerate(ts):
+        arr[i] = None if t is None else t.data_ptr()
+    return arr
+
+
+def stream_of(device=None):
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)

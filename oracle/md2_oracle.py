@@ -1,0 +1,562 @@
+"""CPU restatement of the Monodepth2.jl photometric training step -- TEST INFRASTRUCTURE ONLY.
+
+This module is the parity ORACLE.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import it, and only as the checker / the timed CPU
+baseline.  The product path (``monodepth2.jl_amd/md2hip`` + ``libmd2hip.so``) never imports it
+and fails loudly when the HIP library is missing.
+
+What it restates (reference = jumerckx/Monodepth2.jl @ 2025-01-17, paths relative to the
+reference root).  The reference is Julia/Flux/Zygote and cannot run here (no Julia toolchain,
+no package sources, no network), so autograd is torch-CPU autograd standing
+in for Zygote, and every third-party semantic is an explicit, documented assumption:
+
+  * NNlib ``grid_sample``: bilinear, align_corners=true, ``:border`` clamps coordinates with a
+    zero gradient where clamped -- PINNED by ``test/runtests.jl:94-122`` (identity warp).
+  * NNlib ``upsample_bilinear``: align_corners=true (unpinned).
+  * NNlib ``pad_reflect``: mirror excluding the edge (partially pinned by the SSIM tests).
+  * Flux ``MeanPool((3,3); stride=1)``: no padding, divisor 9.
+  * Flux ``BatchNorm`` train mode: batch mean, biased variance, eps=1e-5, momentum 0.1.
+  * Zygote ``minimum(cat(...); dims=3)``: gradient to the FIRST argmin (ties -> earlier source).
+  * Zygote ``clamp``: gradient 1 on the closed interval [lo, hi]; ``abs'(0) = 0``.
+  * Flux ``ADAM``: eps added to sqrt(v_hat) (``Flux.Optimise.apply!(::ADAM)``), eps=1e-8.
+  * ResNet.jl: torchvision topology (bias-free convs + BN, 7x7/2 stem, 3x3/2 maxpool) -- parity
+    UNPINNED (no reference test touches the encoder).
+
+Tensor conventions (C order, memory-identical to the Julia column-major arrays):
+  Julia (W,H,C,N)      <-> torch [N,C,H,W]
+  Julia x (W,H,C,L,N)  <-> torch [N,L,C,H,W]
+  Julia rvec (3,N)     <-> torch [N,3];  tvec (3,1,N) <-> [N,3];  R (3,3,N) <-> [N,3,3] (R[n,i,j])
+  Julia points (3,W*H,N) <-> torch [N,3,P] with P = H*W, w fastest.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+# ----------------------------------------------------------------------------------------------
+# src/Monodepth.jl:37-60 -- Params / TrainCache
+# ----------------------------------------------------------------------------------------------
+
+
+@dataclass
+class Params:
+    """``Params`` (src/Monodepth.jl:37-47)."""
+    target_size: Tuple[int, int]            # (width, height)
+    batch_size: int
+    min_depth: float = 0.1
+    max_depth: float = 100.0
+    disparity_smoothness: float = 1e-3
+    frame_ids: List[int] = field(default_factory=lambda: [1, 2, 3])
+    automasking: bool = True
+
+
+@dataclass
+class TrainCache:
+    """``TrainCache`` (src/Monodepth.jl:49-60).  ``ssim``/``backprojections``/``projections`` are
+    the stateless helpers below; K / invK are 3x3; ids are 1-based like the reference."""
+    K: torch.Tensor
+    invK: torch.Tensor
+    target_id: int = 2
+    source_ids: Sequence[int] = (1, 3)
+    scales: Sequence[float] = (0.125, 0.25, 0.5, 1.0)
+
+
+def depth10k_K(width: int = 416, height: int = 128, dtype=torch.float64):
+    """Depth10k intrinsics (src/dtk.jl:15-21): f = 2648/4.63461538462, c = (W/2, H/2)."""
+    focal = 2648.0 / 4.63461538462
+    K = torch.tensor([[focal, 0.0, width / 2.0],
+                      [0.0, focal, height / 2.0],
+                      [0.0, 0.0, 1.0]], dtype=torch.float64)
+    invK = torch.linalg.inv(K)
+    return K.to(dtype), invK.to(dtype)
+
+
+# ----------------------------------------------------------------------------------------------
+# src/utils.jl -- geometry + loss primitives
+# ----------------------------------------------------------------------------------------------
+
+
+def pad_reflect(x: torch.Tensor, p: int = 1) -> torch.Tensor:
+    """NNlib ``pad_reflect(x, 1)`` on the two spatial dims (used at src/utils.jl:30-31 and
+    src/depth_decoder.jl:5)."""
+    return F.pad(x, (p, p, p, p), mode="reflect")
+
+
+def ssim(x: torch.Tensor, y: torch.Tensor, c1: float = 0.01 ** 2, c2: float = 0.03 ** 2):
+    """``(ssim::SSIM)(x, y)`` -- src/utils.jl:17-43.  x, y: [N,C,H,W] -> [N,C,H,W]."""
+    xr, yr = pad_reflect(x), pad_reflect(y)
+    pool = lambda t: F.avg_pool2d(t, 3, stride=1)          # MeanPool((3,3); stride=1)
+    mx, my = pool(xr), pool(yr)
+    sx = pool(xr * xr) - mx * mx
+    sy = pool(yr * yr) - my * my
+    sxy = pool(xr * yr) - mx * my
+    n = (2.0 * mx * my + c1) * (2.0 * sxy + c2)
+    d = (mx * mx + my * my + c1) * (sx + sy + c2)
+    return torch.clamp((1.0 - n / d) * 0.5, 0.0, 1.0)
+
+
+def backproject_coordinates(width: int, height: int, dtype=torch.float64):
+    """``Backproject(; width, height)`` cached grid -- src/utils.jl:49-57: 1-based (w, h, 1)."""
+    w = torch.arange(1, width + 1, dtype=dtype).repeat(height)
+    h = torch.arange(1, height + 1, dtype=dtype).repeat_interleave(width)
+    return torch.stack([w, h, torch.ones_like(w)], 0)            # [3, P], w fastest
+
+
+def backproject(depth: torch.Tensor, invK: torch.Tensor, width: int, height: int):
+    """``(b::Backproject)(depth, invK)`` -- src/utils.jl:67-69.  depth [N,1,P] -> [N,3,P]."""
+    coords = backproject_coordinates(width, height, depth.dtype)
+    return depth * (invK.to(depth.dtype) @ coords).unsqueeze(0)
+
+
+def normalize(pixels: torch.Tensor, width: int, height: int):
+    """``normalize(p::Project, pixels)`` -- src/utils.jl:83-85 (1-based pixels -> [-1, 1])."""
+    normalizer = torch.tensor([width - 1.0, height - 1.0], dtype=pixels.dtype).view(1, 2, 1)
+    return (((pixels - 1.0) / normalizer) - 0.5) * 2.0
+
+
+def project(points: torch.Tensor, K: torch.Tensor, R: torch.Tensor, t: torch.Tensor,
+            width: int, height: int):
+    """``(p::Project)(points, K, R, t)`` -- src/utils.jl:99-103.
+    points [N,3,P], K [3,3], R [N,3,3], t [N,3] -> normalized uv [N,2,P]."""
+    cam = K.to(points.dtype) @ (R @ points + t.unsqueeze(-1))
+    denom = 1.0 / (cam[:, 2:3, :] + 1e-7)
+    return normalize(cam[:, 0:2, :] * denom, width, height)
+
+
+def hat(rvec: torch.Tensor) -> torch.Tensor:
+    """``hat`` -- src/utils.jl:123-132 (skew matrix; rrule :134-145 is what autograd gives)."""
+    z = torch.zeros_like(rvec[:, 0])
+    r1, r2, r3 = rvec[:, 0], rvec[:, 1], rvec[:, 2]
+    return torch.stack([
+        torch.stack([z, -r3, r2], -1),
+        torch.stack([r3, z, -r1], -1),
+        torch.stack([-r2, r1, z], -1)], -2)
+
+
+def so3_exp_map(rvec: torch.Tensor) -> torch.Tensor:
+    """``so3_exp_map`` -- src/utils.jl:106-121.  rvec [N,3] -> R [N,3,3].
+    NOTE theta' = max(theta, 1e-4) exactly as the reference (coefficients are not the limits)."""
+    skew = hat(rvec)
+    skew2 = skew @ skew
+    theta = torch.sqrt(torch.sum(rvec * rvec, dim=1))
+    theta_inv = 1.0 / torch.clamp(theta, min=1e-4)
+    f1 = (theta_inv * torch.sin(theta)).view(-1, 1, 1)
+    f2 = (theta_inv * theta_inv * (1.0 - torch.cos(theta))).view(-1, 1, 1)
+    eye = torch.eye(3, dtype=rvec.dtype).unsqueeze(0)
+    return f1 * skew + f2 * skew2 + eye
+
+
+def composeT(rvec: torch.Tensor, t: torch.Tensor, invert: bool):
+    """``composeT`` -- src/utils.jl:185-192.  Returns (R [N,3,3], t [N,3])."""
+    R = so3_exp_map(rvec)
+    if invert:
+        R = R.transpose(1, 2)
+        t = (R @ (-t).unsqueeze(-1)).squeeze(-1)
+    return R, t
+
+
+def smooth_loss(disparity: torch.Tensor, image: torch.Tensor) -> torch.Tensor:
+    """``smooth_loss`` -- src/utils.jl:163-177.  disparity [N,H,W] (Julia WHN), image [N,C,H,W]."""
+    ddx = torch.abs(disparity[:, :, :-1] - disparity[:, :, 1:])
+    ddy = torch.abs(disparity[:, :-1, :] - disparity[:, 1:, :])
+    idx = torch.abs(image[:, :, :, :-1] - image[:, :, :, 1:])
+    idy = torch.abs(image[:, :, :-1, :] - image[:, :, 1:, :])
+    idx = idx.mean(dim=1)
+    idy = idy.mean(dim=1)
+    return torch.mean(ddx * torch.exp(-idx)) + torch.mean(ddy * torch.exp(-idy))
+
+
+def disparity_to_depth(disparity: torch.Tensor, min_depth: float, max_depth: float):
+    """``disparity_to_depth`` -- src/utils.jl:179-183."""
+    min_disp = 1.0 / max_depth
+    max_disp = 1.0 / min_depth
+    return 1.0 / (disparity * (max_disp - min_disp) + min_disp)
+
+
+def grid_sample_border(image: torch.Tensor, grid: torch.Tensor) -> torch.Tensor:
+    """NNlib ``grid_sample(x, grid; padding_mode=:border)`` (src/training.jl:56).
+    image [N,C,H,W], grid [N,H,W,2] with (x, y) normalised, align_corners=true."""
+    return F.grid_sample(image, grid, mode="bilinear", padding_mode="border", align_corners=True)
+
+
+def grid_sample_zeros(image: torch.Tensor, grid: torch.Tensor) -> torch.Tensor:
+    """NNlib ``grid_sample(x, grid)`` default ``padding_mode=:zeros`` (test/runtests.jl:116)."""
+    return F.grid_sample(image, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+
+
+def upsample_bilinear_size(x: torch.Tensor, size_hw: Tuple[int, int]) -> torch.Tensor:
+    """NNlib ``upsample_bilinear(x; size)`` (src/training.jl:45), align_corners=true."""
+    return F.interpolate(x, size=size_hw, mode="bilinear", align_corners=True)
+
+
+def upsample_bilinear_x2(x: torch.Tensor) -> torch.Tensor:
+    """NNlib ``upsample_bilinear(x, (2, 2))`` (src/depth_decoder.jl:18-19), align_corners=true."""
+    return F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=True)
+
+
+# ----------------------------------------------------------------------------------------------
+# src/training.jl -- objective
+# ----------------------------------------------------------------------------------------------
+
+
+def _first_argmin(losses: Sequence[torch.Tensor]) -> torch.Tensor:
+    """``minimum(cat(...; dims=3); dims=3)`` with Zygote's first-argmin adjoint."""
+    out = losses[0]
+    for l in losses[1:]:
+        out = torch.where(l < out, l, out)
+    return out
+
+
+def photometric_loss(predicted: torch.Tensor, target: torch.Tensor, alpha: float = 0.85):
+    """``photometric_loss`` -- src/training.jl:1-7.  -> [N,1,H,W]."""
+    l1 = torch.mean(torch.abs(target - predicted), dim=1, keepdim=True)
+    s = torch.mean(ssim(predicted, target), dim=1, keepdim=True)
+    return alpha * s + (1.0 - alpha) * l1
+
+
+def automasking_loss(inputs: torch.Tensor, target: torch.Tensor, source_ids: Sequence[int]):
+    """``automasking_loss`` -- src/training.jl:9-11.  inputs [N,L,C,H,W]; ids 1-based."""
+    return _first_argmin([photometric_loss(inputs[:, i - 1], target) for i in source_ids])
+
+
+def prediction_loss(predictions: Sequence[torch.Tensor], target: torch.Tensor):
+    """``prediction_loss`` -- src/training.jl:13-15."""
+    return _first_argmin([photometric_loss(p, target) for p in predictions])
+
+
+def apply_mask(mask: torch.Tensor, warp_loss: torch.Tensor):
+    """``_apply_mask`` -- src/training.jl:17-19 (mask first in the cat => ties go to the mask)."""
+    return _first_argmin([mask, warp_loss])
+
+
+def warp(disparity_full, x, Ps, K, invK, source_ids, min_depth, max_depth):
+    """The per-scale warp body of ``train_loss`` (src/training.jl:48-57).  Also the definition of
+    the ``warp`` that ``slow_depth`` calls but the reference never defines (defect D1).
+    disparity_full [N,1,H,W]; x [N,L,C,H,W]; Ps = [(R [N,3,3], t [N,3])] per source."""
+    N, _, H, W = disparity_full.shape
+    depth = disparity_to_depth(disparity_full, min_depth, max_depth)
+    coords = backproject(depth.reshape(N, 1, H * W), invK, W, H)
+    warped = []
+    for (R, t), sid in zip(Ps, source_ids):
+        uv = project(coords, K, R, t, W, H)                       # [N,2,P]
+        grid = uv.reshape(N, 2, H, W).permute(0, 2, 3, 1)         # [N,H,W,2]
+        warped.append(grid_sample_border(x[:, sid - 1], grid))
+    return warped
+
+
+def poses_to_transforms(poses, source_ids, target_id):
+    """src/training.jl:29-32: inverse_transform = source_ids .< target_id."""
+    return [composeT(rvec, tvec, sid < target_id) for (rvec, tvec), sid in zip(poses, source_ids)]
+
+
+def _forced_min(cands: Sequence[torch.Tensor], sel: torch.Tensor) -> torch.Tensor:
+    """Test hook: the min over candidates with the argmin imposed (sel[p] = chosen index, where
+    index 0 is the automask when present).  Same value as _first_argmin wherever the choice is
+    unambiguous; lets parity be checked tightly at fp32-vs-fp64 near-ties."""
+    out = torch.zeros_like(cands[0])
+    for i, c in enumerate(cands):
+        out = torch.where(sel == i, c, out)
+    return out
+
+
+def loss_from_outputs(disparities, poses, x, auto_loss, cache: TrainCache, params: Params,
+                      return_parts: bool = False, forced_sel=None, per_source=None):
+    """The body of ``train_loss`` after the model call -- src/training.jl:25,29-77.
+    disparities: list of [N,1,h,w] (one per scale); poses: list of (rvec [N,3], tvec [N,3])."""
+    width, height = params.target_size
+    target_x = x[:, cache.target_id - 1]
+    Ps = poses_to_transforms(poses, cache.source_ids, cache.target_id)
+    loss = torch.zeros((), dtype=x.dtype)
+    parts = []
+    for disparity, scale in zip(disparities, cache.scales):
+        if disparity.shape[-1] != width or disparity.shape[-2] != height:
+            disparity = upsample_bilinear_size(disparity, (height, width))
+        warped = warp(disparity, x, Ps, cache.K, cache.invK, cache.source_ids,
+                      params.min_depth, params.max_depth)
+        src_losses = [photometric_loss(p, target_x) for p in warped]
+        if per_source is not None:
+            per_source.append([l.detach() for l in src_losses])
+        if forced_sel is not None:
+            cands = ([auto_loss] if params.automasking else []) + src_losses
+            warp_loss = _forced_min(cands, forced_sel[len(parts)])
+        else:
+            warp_loss = _first_argmin(src_losses)
+            if params.automasking:
+                warp_loss = apply_mask(auto_loss, warp_loss)
+        normalized = disparity / (disparity.mean(dim=(2, 3), keepdim=True) + 1e-7)
+        disparity_loss = smooth_loss(normalized[:, 0], target_x) * params.disparity_smoothness * scale
+        term_w, term_s = torch.mean(warp_loss), disparity_loss
+        parts.append((term_w, term_s))
+        loss = loss + term_w + term_s
+    loss = loss / len(cache.scales)
+    return (loss, parts) if return_parts else loss
+
+
+# ----------------------------------------------------------------------------------------------
+# Models: ResNet encoder (ext ResNet.jl, torchvision topology), DepthDecoder, PoseDecoder, Model
+# ----------------------------------------------------------------------------------------------
+
+RESNET_LAYERS = {18: (2, 2, 2, 2), 34: (3, 4, 6, 3), 50: (3, 4, 6, 3)}
+
+
+def encoder_stage_channels(arch: int) -> List[int]:
+    """``encoder.stages`` of ResNet.jl (scripts/script.jl:78; channel maths of
+    src/depth_decoder.jl:31-35)."""
+    return [64, 64, 128, 256, 512] if arch in (18, 34) else [64, 256, 512, 1024, 2048]
+
+
+def param_spec(arch: int = 18, in_channels: int = 3, scale_levels=(2, 3, 4, 5),
+               embedding_levels: int = 0):
+    """The flat parameter order the HIP library uses (mirrors ``md2_arch_param_table``):
+    list of (name, shape).  Conv weights are cross-correlation [Cout,Cin,KH,KW]."""
+    spec = []
+
+    def conv(name, cin, cout, k, bias):
+        spec.append((name + ".weight", (cout, cin, k, k)))
+        if bias:
+            spec.append((name + ".bias", (cout,)))
+
+    def bn(name, c):
+        spec.append((name + ".gamma", (c,)))
+        spec.append((name + ".beta", (c,)))
+
+    # encoder
+    conv("encoder.stem.conv", in_channels, 64, 7, False)
+    bn("encoder.stem.bn", 64)
+    layers = RESNET_LAYERS[arch]
+    bottleneck = arch >= 50
+    exp = 4 if bottleneck else 1
+    cin = 64
+    for si, (nblocks, width) in enumerate(zip(layers, (64, 128, 256, 512))):
+        for bi in range(nblocks):
+            stride = 2 if (bi == 0 and si > 0) else 1
+            p = f"encoder.layer{si + 1}.{bi}"
+            cout = width * exp
+            if bottleneck:
+                conv(p + ".conv1", cin, width, 1, False); bn(p + ".bn1", width)
+                conv(p + ".conv2", width, width, 3, False); bn(p + ".bn2", width)
+                conv(p + ".conv3", width, cout, 1, False); bn(p + ".bn3", cout)
+            else:
+                conv(p + ".conv1", cin, width, 3, False); bn(p + ".bn1", width)
+                conv(p + ".conv2", width, width, 3, False); bn(p + ".bn2", width)
+            if stride != 1 or cin != cout:
+                conv(p + ".down", cin, cout, 1, False); bn(p + ".down_bn", cout)
+            cin = cout
+    # depth decoder (src/depth_decoder.jl:26-50)
+    enc = encoder_stage_channels(arch)
+    dec = [256, 128, 64, 32, 16]
+    encr = [c + embedding_levels for c in enc[::-1]]
+    in_ch = [encr[0]] + dec[:-1]
+    skip = encr[1:] + [0]
+    bstart = 1
+    for li, slevel in enumerate(scale_levels):
+        for bid in range(bstart, slevel + 1):
+            b = bid - 1
+            conv(f"depth.branch{bid}.c1", in_ch[b], dec[b], 3, True)
+            conv(f"depth.branch{bid}.c2", dec[b] + skip[b], dec[b], 3, True)
+        conv(f"depth.head{slevel}", dec[slevel - 1], 1, 3, True)
+        bstart = slevel + 1
+    # pose decoder (src/pose_decoder.jl:13-21)
+    conv("pose.squeezer", enc[-1], 256, 1, True)
+    conv("pose.conv1", 512, 256, 3, True)
+    conv("pose.conv2", 256, 256, 3, True)
+    conv("pose.conv3", 256, 6, 1, True)
+    return spec
+
+
+def init_params(spec, seed: int = 42, dtype=torch.float64) -> torch.Tensor:
+    """Flux defaults: glorot_uniform conv weights (fan over kh*kw*cin / kh*kw*cout), zero bias,
+    BN gamma=1 beta=0.  Returns the flat parameter vector (float64)."""
+    g = torch.Generator().manual_seed(seed)
+    chunks = []
+    for name, shape in spec:
+        if name.endswith(".weight"):
+            cout, cin, kh, kw = shape
+            fan_in, fan_out = cin * kh * kw, cout * kh * kw
+            lim = math.sqrt(6.0 / (fan_in + fan_out))
+            chunks.append((torch.rand(shape, generator=g, dtype=torch.float64) * 2 - 1) * lim)
+        elif name.endswith(".gamma"):
+            chunks.append(torch.ones(shape, dtype=torch.float64))
+        else:
+            chunks.append(torch.zeros(shape, dtype=torch.float64))
+    return torch.cat([c.reshape(-1) for c in chunks]).to(dtype)
+
+
+def unflatten(flat: torch.Tensor, spec):
+    out, off = {}, 0
+    for name, shape in spec:
+        n = 1
+        for s in shape:
+            n *= s
+        out[name] = flat[off:off + n].view(shape)
+        off += n
+    assert off == flat.numel()
+    return out
+
+
+def batchnorm_train(x, gamma, beta, eps=1e-5):
+    """Flux ``BatchNorm`` in train mode (``trainmode!``, scripts/script.jl:86)."""
+    return F.batch_norm(x, None, None, gamma, beta, training=True, momentum=0.1, eps=eps)
+
+
+def resnet_stages(P, x, arch=18):
+    """ResNet.jl ``encoder(x, Val(:stages))`` (src/model.jl:37) -> 5 stage features."""
+    y = F.conv2d(x, P["encoder.stem.conv.weight"], stride=2, padding=3)
+    y = F.relu(batchnorm_train(y, P["encoder.stem.bn.gamma"], P["encoder.stem.bn.beta"]))
+    feats = [y]
+    y = F.max_pool2d(y, 3, stride=2, padding=1)
+    layers = RESNET_LAYERS[arch]
+    bottleneck = arch >= 50
+    for si, nblocks in enumerate(layers):
+        for bi in range(nblocks):
+            stride = 2 if (bi == 0 and si > 0) else 1
+            p = f"encoder.layer{si + 1}.{bi}"
+            if bottleneck:
+                h = F.relu(batchnorm_train(F.conv2d(y, P[p + ".conv1.weight"]), P[p + ".bn1.gamma"], P[p + ".bn1.beta"]))
+                h = F.relu(batchnorm_train(F.conv2d(h, P[p + ".conv2.weight"], stride=stride, padding=1), P[p + ".bn2.gamma"], P[p + ".bn2.beta"]))
+                h = batchnorm_train(F.conv2d(h, P[p + ".conv3.weight"]), P[p + ".bn3.gamma"], P[p + ".bn3.beta"])
+            else:
+                h = F.relu(batchnorm_train(F.conv2d(y, P[p + ".conv1.weight"], stride=stride, padding=1), P[p + ".bn1.gamma"], P[p + ".bn1.beta"]))
+                h = batchnorm_train(F.conv2d(h, P[p + ".conv2.weight"], padding=1), P[p + ".bn2.gamma"], P[p + ".bn2.beta"])
+            if (p + ".down.weight") in P:
+                idn = batchnorm_train(F.conv2d(y, P[p + ".down.weight"], stride=stride), P[p + ".down_bn.gamma"], P[p + ".down_bn.beta"])
+            else:
+                idn = y
+            y = F.relu(h + idn)
+        feats.append(y)
+    return feats
+
+
+def _decoder_block(P, name, x, act):
+    """``DecoderBlock`` = pad_reflect(1) + valid 3x3 Conv (src/depth_decoder.jl:1-5)."""
+    y = F.conv2d(pad_reflect(x), P[name + ".weight"], P[name + ".bias"])
+    return act(y)
+
+
+def depth_decoder(P, features, scale_levels=(2, 3, 4, 5)):
+    """``(d::DepthDecoder)(features)`` -- src/depth_decoder.jl:52-68 (BranchBlock :7-19)."""
+    x, skips = features[-1], features[:-1][::-1]
+    outs, bstart = [], 1
+    for slevel in scale_levels:
+        for bid in range(bstart, slevel + 1):
+            y = _decoder_block(P, f"depth.branch{bid}.c1", x, F.elu)
+            y = upsample_bilinear_x2(y)
+            if bid <= len(skips):
+                y = torch.cat([y, skips[bid - 1]], dim=1)
+            x = _decoder_block(P, f"depth.branch{bid}.c2", y, F.elu)
+        outs.append(_decoder_block(P, f"depth.head{slevel}", x, torch.sigmoid))
+        bstart = slevel + 1
+    return outs
+
+
+def pose_decoder(P, fa, fb):
+    """``(decoder::PoseDecoder)(features)`` -- src/pose_decoder.jl:23-32."""
+    sq = lambda f: F.relu(F.conv2d(f, P["pose.squeezer.weight"], P["pose.squeezer.bias"]))
+    y = torch.cat([sq(fa), sq(fb)], dim=1)
+    y = F.relu(F.conv2d(y, P["pose.conv1.weight"], P["pose.conv1.bias"], padding=1))
+    y = F.relu(F.conv2d(y, P["pose.conv2.weight"], P["pose.conv2.bias"], padding=1))
+    y = F.conv2d(y, P["pose.conv3.weight"], P["pose.conv3.bias"])
+    pose = 1e-2 * y.mean(dim=(2, 3))                               # [N,6]
+    return pose[:, 0:3], pose[:, 3:6]
+
+
+def model_forward(P, x, source_ids=(1, 3), target_id=2, arch=18, scale_levels=(2, 3, 4, 5)):
+    """Mono-mode ``(m::Model)(x, source_ids, target_id)`` (src/model.jl:31-55 without the MPI
+    embedding; defect D2 makes MPI mode shape-inconsistent for B>1).  x [N,L,C,H,W]."""
+    N, L, C, H, W = x.shape
+    feats = resnet_stages(P, x.reshape(N * L, C, H, W), arch)
+    feats = [f.reshape(N, L, *f.shape[1:]) for f in feats]
+    disps = depth_decoder(P, [f[:, target_id - 1] for f in feats], scale_levels)
+    poses = []
+    for i in source_ids:                                           # eval_poses, src/model.jl:57-70
+        if i < target_id:
+            fa, fb = feats[-1][:, i - 1], feats[-1][:, target_id - 1]
+        else:
+            fa, fb = feats[-1][:, target_id - 1], feats[-1][:, i - 1]
+        poses.append(pose_decoder(P, fa, fb))
+    return disps, poses
+
+
+def eval_disparity(P, x, arch=18, scale_levels=(2, 3, 4, 5)):
+    """``eval_disparity(m, x)`` -- src/model.jl:63.  x [N,C,H,W]."""
+    return depth_decoder(P, resnet_stages(P, x, arch), scale_levels)
+
+
+def train_loss(P, x, auto_loss, cache: TrainCache, params: Params, arch=18,
+               scale_levels=(2, 3, 4, 5)):
+    """``train_loss`` -- src/training.jl:21-78 (returns the scalar loss)."""
+    disps, poses = model_forward(P, x, cache.source_ids, cache.target_id, arch, scale_levels)
+    return loss_from_outputs(disps, poses, x, auto_loss, cache, params)
+
+
+# ----------------------------------------------------------------------------------------------
+# MPI-mode helpers (src/model.jl:1-22) -- forward parity only
+# ----------------------------------------------------------------------------------------------
+
+
+def embed(x: torch.Tensor, L: int = 10) -> torch.Tensor:
+    """``embed`` -- src/model.jl:4-15.  x [B, num_bins] (Julia num_bins x batch) ->
+    [B, num_bins, 2L+1] (Julia (1,1,2L+1,num_bins,batch))."""
+    parts = [x]
+    for i in range(L):
+        parts += [torch.sin(2.0 ** i * x), torch.cos(2.0 ** i * x)]
+    return torch.stack(parts, -1)
+
+
+def disparity_bins(num_bins: int, u: torch.Tensor, near=1.0, far=0.001):
+    """``uniformly_sample_disparity_from_linspace_bins`` -- src/model.jl:17-21, with the
+    CURAND draw (defect D3) injected as ``u`` [B, num_bins] in [0,1)."""
+    edges = torch.linspace(near, far, num_bins + 1, dtype=u.dtype)[:-1]
+    interval = edges[1] - edges[0]
+    return edges.unsqueeze(0) + u * interval
+
+
+# ----------------------------------------------------------------------------------------------
+# Optimiser -- Flux ADAM (scripts/script.jl:85, src/simple_depth.jl:16)
+# ----------------------------------------------------------------------------------------------
+
+
+class Adam:
+    """Flux ``ADAM(eta, (0.9, 0.999))``: m,v moments, bias-corrected, eps on sqrt(v_hat)."""
+
+    def __init__(self, eta=1e-4, beta=(0.9, 0.999), eps=1e-8):
+        self.eta, self.beta, self.eps = eta, beta, eps
+        self.state = {}
+
+    def step(self, key, x: torch.Tensor, g: torch.Tensor):
+        if key not in self.state:
+            self.state[key] = [torch.zeros_like(x), torch.zeros_like(x), [self.beta[0], self.beta[1]]]
+        m, v, bp = self.state[key]
+        m.mul_(self.beta[0]).add_((1 - self.beta[0]) * g)
+        v.mul_(self.beta[1]).add_((1 - self.beta[1]) * g * g)
+        delta = m / (1 - bp[0]) / (torch.sqrt(v / (1 - bp[1])) + self.eps) * self.eta
+        bp[0] *= self.beta[0]
+        bp[1] *= self.beta[1]
+        x.sub_(delta)
+
+
+# ----------------------------------------------------------------------------------------------
+# Config 1: slow_depth (src/simple_depth.jl:1-62), with warp := training.jl:48-57
+# ----------------------------------------------------------------------------------------------
+
+
+def slow_depth_loss(disp, rvecs, tvecs, x, K, invK, source_ids=(1, 3), target_id=2,
+                    min_depth=0.1, max_depth=100.0):
+    """Loss inside the ``gradient(theta)`` closure of ``slow_depth`` (src/simple_depth.jl:25-41):
+    mean(prediction_loss) + smooth_loss(disp) (no 1e-3 weight, no mean normalisation)."""
+    Ps = [composeT(r, t, sid < target_id) for r, t, sid in zip(rvecs, tvecs, source_ids)]
+    warped = warp(disp, x, Ps, K, invK, source_ids, min_depth, max_depth)
+    target_x = x[:, target_id - 1]
+    return torch.mean(prediction_loss(warped, target_x)) + smooth_loss(disp[:, 0], target_x)
+
+
+def slow_depth_init(width, height, dtype=torch.float64):
+    """src/simple_depth.jl:8-13: disp = 0.5, rvec = [0,0,0.01], tvec = 0 per source."""
+    disp = torch.full((1, 1, height, width), 0.5, dtype=dtype)
+    rvecs = [torch.tensor([[0.0, 0.0, 0.01]], dtype=dtype) for _ in range(2)]
+    tvecs = [torch.zeros(1, 3, dtype=dtype) for _ in range(2)]
+    return disp, rvecs, tvecs
