@@ -92,6 +92,30 @@ int md2_so3_compose_fwd(const float* pose, int n, int invert_mask, float* Rt, vo
 int md2_so3_compose_bwd(const float* pose, int n, int invert_mask, const float* dRt,
                         float* d_pose, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * 2-D convolution (Flux Conv / NNlib conv, ∇conv_data, ∇conv_filter) on gfx950 fp32 MFMA.
+ * x [n][cin][h][w], w [cout][cin][kh][kw] (cross-correlation; flip Flux kernels), bias [cout],
+ * y [n][cout][ho][wo].  reflect=1: NNlib pad_reflect(x, pad) then a valid conv
+ * (src/depth_decoder.jl:5; 3x3, stride 1, pad 1 only).  act: 0 none, 1 relu, 2 elu, 3 sigmoid.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct md2_conv_desc {
+  int n, cin, h, w, cout, kh, kw, stride, pad, reflect;
+  int act;
+} md2_conv_desc;
+
+size_t md2_conv2d_workspace_size(const md2_conv_desc* d);
+int md2_conv2d_fwd(const md2_conv_desc* d, const float* x, const float* w, const float* bias,
+                   float* y, void* workspace, void* stream);
+/* dx = ∇conv_data(dy_pre) where dy_pre is the gradient w.r.t. the pre-activation output. */
+int md2_conv2d_dgrad(const md2_conv_desc* d, const float* dy, const float* w, float* dx,
+                     void* workspace, void* stream);
+/* dw = ∇conv_filter(x, dy_pre), db = sum(dy_pre) (db may be NULL). */
+int md2_conv2d_wgrad(const md2_conv_desc* d, const float* x, const float* dy, float* dw,
+                     float* db, void* workspace, void* stream);
+/* dpre = dout .* act'(out) from the stored post-activation output (n elements). */
+int md2_act_backward(const float* out, const float* dout, float* dpre, long long n, int act,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4,7 +4,10 @@
 #include <cstring>
 #include <string>
 
+#include "conv.h"
 #include "loss_tail.h"
+
+#include <algorithm>
 
 namespace md2 {
 static thread_local std::string g_last_error;
@@ -83,6 +86,88 @@ int md2_so3_compose_bwd(const float* pose, int n, int invert_mask, const float* 
                         float* d_pose, void* stream) {
   MD2_CHECK_ARG(pose && dRt && d_pose && n > 0, "so3 bwd args");
   return launch_so3_bwd(pose, 2 * n, n, invert_mask, dRt, d_pose, 0, (hipStream_t)stream);
+}
+
+static ConvShape to_shape(const md2_conv_desc* d) {
+  ConvShape s{};
+  s.N = d->n;
+  s.Cin = d->cin;
+  s.H = d->h;
+  s.W = d->w;
+  s.Cout = d->cout;
+  s.KH = d->kh;
+  s.KW = d->kw;
+  s.stride = d->stride;
+  s.pad = d->pad;
+  s.reflect = d->reflect;
+  s.Ho = (d->h + 2 * d->pad - d->kh) / d->stride + 1;
+  s.Wo = (d->w + 2 * d->pad - d->kw) / d->stride + 1;
+  return s;
+}
+
+static size_t align_up(size_t b) { return (b + 255) & ~size_t(255); }
+
+size_t md2_conv2d_workspace_size(const md2_conv_desc* d) {
+  if (!d) return 0;
+  const ConvShape s = to_shape(d);
+  size_t packed = std::max(conv_fwd_packed_elems(s), conv_dgrad_packed_elems(s)) * sizeof(float);
+  size_t slab = std::max(conv_fwd_workspace(s), std::max(conv_dgrad_workspace(s), conv_wgrad_workspace(s)));
+  return align_up(packed) + align_up(slab);
+}
+
+int md2_conv2d_fwd(const md2_conv_desc* d, const float* x, const float* w, const float* bias,
+                   float* y, void* workspace, void* stream) {
+  MD2_CHECK_ARG(d && x && w && y && workspace, "conv2d_fwd args");
+  const ConvShape s = to_shape(d);
+  hipStream_t st = (hipStream_t)stream;
+  float* packed = (float*)workspace;
+  const size_t pbytes = align_up(std::max(conv_fwd_packed_elems(s), conv_dgrad_packed_elems(s)) * sizeof(float));
+  MD2_TRY(conv_pack_fwd(s, w, packed, st));
+  TensorIn in;
+  in.p0 = x;
+  in.c0 = s.Cin;
+  in.bs0 = (long)s.Cin * s.H * s.W;
+  TensorOut out;
+  out.p0 = y;
+  out.bs0 = (long)s.Cout * s.Ho * s.Wo;
+  out.bias = bias;
+  out.act = d->act;
+  ConvWorkspace ws{(char*)workspace + pbytes, md2_conv2d_workspace_size(d) - pbytes};
+  return conv_fwd(s, in, packed, out, ws, st);
+}
+
+int md2_conv2d_dgrad(const md2_conv_desc* d, const float* dy, const float* w, float* dx,
+                     void* workspace, void* stream) {
+  MD2_CHECK_ARG(d && dy && w && dx && workspace, "conv2d_dgrad args");
+  const ConvShape s = to_shape(d);
+  hipStream_t st = (hipStream_t)stream;
+  float* packed = (float*)workspace;
+  const size_t pbytes = align_up(std::max(conv_fwd_packed_elems(s), conv_dgrad_packed_elems(s)) * sizeof(float));
+  MD2_TRY(conv_pack_dgrad(s, w, packed, st));
+  TensorOut out;
+  out.p0 = dx;
+  out.bs0 = (long)s.Cin * s.H * s.W;
+  ConvWorkspace ws{(char*)workspace + pbytes, md2_conv2d_workspace_size(d) - pbytes};
+  return conv_dgrad(s, dy, packed, out, ws, st);
+}
+
+int md2_conv2d_wgrad(const md2_conv_desc* d, const float* x, const float* dy, float* dw,
+                     float* db, void* workspace, void* stream) {
+  MD2_CHECK_ARG(d && x && dy && dw && workspace, "conv2d_wgrad args");
+  const ConvShape s = to_shape(d);
+  const size_t pbytes = align_up(std::max(conv_fwd_packed_elems(s), conv_dgrad_packed_elems(s)) * sizeof(float));
+  TensorIn in;
+  in.p0 = x;
+  in.c0 = s.Cin;
+  in.bs0 = (long)s.Cin * s.H * s.W;
+  ConvWorkspace ws{(char*)workspace + pbytes, md2_conv2d_workspace_size(d) - pbytes};
+  return conv_wgrad(s, in, dy, dw, db, 0, ws, (hipStream_t)stream);
+}
+
+int md2_act_backward(const float* out, const float* dout, float* dpre, long long n, int act,
+                     void* stream) {
+  MD2_CHECK_ARG(out && dout && dpre && n >= 0, "act_backward args");
+  return act_backward(out, dout, dpre, (long)n, act, (hipStream_t)stream);
 }
 
 }  // extern "C"

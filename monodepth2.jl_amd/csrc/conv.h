@@ -1,0 +1,72 @@
+// Implicit-GEMM 2-D convolution on gfx950 fp32 MFMA: forward, data-gradient, filter-gradient.
+//
+// Replaces NNlib conv / ∇conv_data / ∇conv_filter behind Flux `Conv` (src/depth_decoder.jl:13-14,
+// 46; src/pose_decoder.jl:15-19; the ResNet.jl encoder).  Weights are stored as cross-correlation
+// kernels [Cout][Cin][KH][KW] (the Julia shim flips Flux's true-convolution kernels).
+#pragma once
+#include "common.h"
+
+namespace md2 {
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2, ACT_SIGMOID = 3 };
+
+struct ConvShape {
+  int N;            // images
+  int Cin, H, W;    // input
+  int Cout, Ho, Wo; // output
+  int KH, KW, stride, pad;
+  int reflect;      // 1: NNlib pad_reflect(x, pad) + valid conv (src/depth_decoder.jl:5)
+};
+
+// Input operand: channel concat of up to two tensors (cat(..., dims=3)), each [img][c][H][W].
+// p0 image offset = (b % bdiv) * bs0 + (b / bdiv) * bhi  (lets the stem read x[n][l] frames
+// in frame-major encoder order); p1 image offset = b * bs1.
+struct TensorIn {
+  const float* p0 = nullptr;
+  const float* p1 = nullptr;
+  int c0 = 0;          // channels held by p0 (== Cin when p1 is unused)
+  long bs0 = 0, bs1 = 0;
+  int bdiv = 1 << 30;
+  long bhi = 0;
+};
+
+// Output: rows m < c0 go to p0, the rest to p1 (channel split for the concat gradient).
+struct TensorOut {
+  float* p0 = nullptr;
+  float* p1 = nullptr;
+  int c0 = 1 << 30;
+  long bs0 = 0, bs1 = 0;   // image strides
+  const float* bias = nullptr;
+  int act = ACT_NONE;
+  int accumulate = 0;      // out += result
+};
+
+struct ConvWorkspace {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+
+// packed operand sizes (elements) -- weights are repacked K-major with zero padding
+size_t conv_fwd_packed_elems(const ConvShape& s);
+size_t conv_dgrad_packed_elems(const ConvShape& s);
+int conv_pack_fwd(const ConvShape& s, const float* w, float* packed, hipStream_t st);
+int conv_pack_dgrad(const ConvShape& s, const float* w, float* packed, hipStream_t st);
+
+// workspace needed for split-K slabs (bytes)
+size_t conv_fwd_workspace(const ConvShape& s);
+size_t conv_dgrad_workspace(const ConvShape& s);
+size_t conv_wgrad_workspace(const ConvShape& s);
+
+int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const TensorOut& y,
+             ConvWorkspace ws, hipStream_t st);
+// dX from dY (dY: [N][Cout][Ho][Wo] pre-activation gradient)
+int conv_dgrad(const ConvShape& s, const float* dy, const float* wpacked_d, const TensorOut& dx,
+               ConvWorkspace ws, hipStream_t st);
+// dW [Cout][Cin*KH*KW] (store or accumulate) and optional db [Cout]
+int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw, float* db,
+               int accumulate, ConvWorkspace ws, hipStream_t st);
+
+// dPre = dOut * act'(out) (act from the stored post-activation output), elementwise
+int act_backward(const float* out, const float* dout, float* dpre, long n, int act, hipStream_t st);
+
+}  // namespace md2

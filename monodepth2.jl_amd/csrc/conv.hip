@@ -1,0 +1,732 @@
+// Implicit-GEMM convolution kernels for gfx950 (see conv.h).
+//
+// All three passes are one GEMM shape  C[M][N] = sum_k A[k][m] * B[k][n]  computed with the
+// exact-fp32 MFMA v_mfma_f32_32x32x2_f32 (64 lanes: A[i=l&31][k=l>>5], B[k=l>>5][j=l&31]; C/D:
+// col j = lane&31, row i = (r&3) + 8(r>>2) + 4(lane>>5)).  The N (lane) dimension is always the
+// pixel or filter-column axis, so every epilogue store writes 32 consecutive floats per register.
+//
+//   forward : M = Cout, N = images*Ho*Wo,  K = Cin*KH*KW     A = packed W^T,  B = im2col(x)
+//   dgrad   : M = Cin,  N = images*H*W,    K = Cout*KH*KW    A = packed W,    B = gather(dY)
+//   wgrad   : M = Cout, N = Cin*KH*KW,     K = images*Ho*Wo  A = dY^T,        B = im2col(x)^T
+//
+// Tiles are staged global -> registers -> LDS (double buffered, one barrier per K step); the
+// im2col / gather address maths runs on SALU (wave-uniform k decode) and VALU in the shadow of
+// the 64-cycle f32 MFMAs.  Small-M / huge-K shapes (layer4, wgrad) use split-K slabs reduced by
+// a second kernel that also applies the epilogue (deterministic, no atomics).
+#include "conv.h"
+
+namespace md2 {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int KPAD = 32;    // packed weight K padding
+constexpr int MPAD = 128;   // packed weight M padding
+
+static inline long round_up(long a, long b) { return (a + b - 1) / b * b; }
+
+__device__ __forceinline__ int refl(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return fmaxf(v, 0.f);
+    case ACT_ELU: return v > 0.f ? v : expm1f(v);
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    default: return v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight packing
+// ---------------------------------------------------------------------------------------------
+// forward:  Wt[k][m] = W[m][k],               k = ci*KK + kh*KW + kw     ([Kpad][Mpad])
+__global__ void pack_fwd_kernel(const float* __restrict__ w, float* __restrict__ out, int M, int K,
+                                int Kpad, int Mpad) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)Kpad * Mpad) return;
+  const int k = (int)(idx / Mpad), m = (int)(idx % Mpad);
+  out[idx] = (k < K && m < M) ? w[(long)m * K + k] : 0.f;
+}
+
+// dgrad:    Wd[k'][ci] = W[co][ci][kh][kw],   k' = co*KK + kh*KW + kw    ([Kdpad][Cinpad])
+__global__ void pack_dgrad_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout,
+                                  int Cin, int KK, int Kpad, int Mpad) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)Kpad * Mpad) return;
+  const int k = (int)(idx / Mpad), ci = (int)(idx % Mpad);
+  float v = 0.f;
+  if (k < Cout * KK && ci < Cin) {
+    const int co = k / KK, r = k % KK;
+    v = w[((long)co * Cin + ci) * KK + r];
+  }
+  out[idx] = v;
+}
+
+size_t conv_fwd_packed_elems(const ConvShape& s) {
+  return (size_t)round_up((long)s.Cin * s.KH * s.KW, KPAD) * round_up(s.Cout, MPAD);
+}
+size_t conv_dgrad_packed_elems(const ConvShape& s) {
+  return (size_t)round_up((long)s.Cout * s.KH * s.KW, KPAD) * round_up(s.Cin, MPAD);
+}
+
+int conv_pack_fwd(const ConvShape& s, const float* w, float* packed, hipStream_t st) {
+  const int K = s.Cin * s.KH * s.KW;
+  const int Kpad = (int)round_up(K, KPAD), Mpad = (int)round_up(s.Cout, MPAD);
+  const long total = (long)Kpad * Mpad;
+  hipLaunchKernelGGL(pack_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, w, packed, s.Cout,
+                     K, Kpad, Mpad);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int conv_pack_dgrad(const ConvShape& s, const float* w, float* packed, hipStream_t st) {
+  const int KK = s.KH * s.KW;
+  const int Kpad = (int)round_up((long)s.Cout * KK, KPAD), Mpad = (int)round_up(s.Cin, MPAD);
+  const long total = (long)Kpad * Mpad;
+  hipLaunchKernelGGL(pack_dgrad_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, w, packed,
+                     s.Cout, s.Cin, KK, Kpad, Mpad);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// kernel arguments
+// ---------------------------------------------------------------------------------------------
+struct GemmDims {
+  int M;
+  long N;       // pixels (fwd/dgrad) or filter columns (wgrad)
+  int K;        // reduction length (fwd/dgrad); wgrad: pixels (long fits int here)
+  int kper;     // K elements per split (multiple of BK)
+  int Mpad;     // packed A leading dimension (fwd/dgrad)
+};
+
+struct ConvArgs {
+  GemmDims g;
+  int Cin, H, W, Cout, Ho, Wo, stride, pad;
+  long HW, HoWo;
+  FastDiv fd_pix;    // pixels per image of the N axis (Ho*Wo fwd/wgrad, H*W dgrad)
+  FastDiv fd_row;    // row length of the N axis (Wo fwd/wgrad, W dgrad)
+  FastDiv fd_bdiv;
+  TensorIn in;
+  const float* A;    // packed weights (fwd/dgrad)
+  const float* dy;   // dgrad / wgrad
+  TensorOut out;
+  float* slab;       // split-K partials [splits][M][N] or nullptr
+};
+
+template <int TM, int TN, int BK>
+__device__ __forceinline__ void mma_chunk(const float* __restrict__ As, int lda,
+                                          const float* __restrict__ Bs, int ldb, int am0, int bn0,
+                                          int lane, f32x16 (&acc)[TM][TN]) {
+  const int kh = lane >> 5, l = lane & 31;
+#pragma unroll
+  for (int kk = 0; kk < BK / 2; ++kk) {
+    float a[TM], b[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = As[(2 * kk + kh) * lda + am0 + i * 32 + l];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b[j] = Bs[(2 * kk + kh) * ldb + bn0 + j * 32 + l];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// Epilogue of one accumulator element (m, n) for the NCHW-style outputs of fwd / dgrad.
+__device__ __forceinline__ void store_out(const TensorOut& o, int m, int img, long pix, long HoWo,
+                                          float v) {
+  if (o.bias) v += o.bias[m];
+  v = apply_act(v, o.act);
+  float* dst = (m < o.c0) ? o.p0 + (long)img * o.bs0 + (long)m * HoWo + pix
+                          : o.p1 + (long)img * o.bs1 + (long)(m - o.c0) * HoWo + pix;
+  if (o.accumulate)
+    *dst += v;
+  else
+    *dst = v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward / dgrad kernel (B operand lanes along pixels)
+// MODE 0 = forward (im2col of x), MODE 1 = dgrad (gather of dY)
+// ---------------------------------------------------------------------------------------------
+template <int MODE, int BM, int BN, int BK, int WM, int WN, int KH, int KW, int S, int RFL>
+__global__ __launch_bounds__(256) void conv_px_kernel(ConvArgs a) {
+  constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN);
+  constexpr int KK = KH * KW;
+  constexpr int A_TOT = BK * BM / 4;
+  constexpr int A_F4 = (A_TOT + 255) / 256;
+  constexpr int B_RS = 256 / BN;
+  constexpr int B_EL = BK / B_RS;
+  static_assert(A_F4 >= 1 && B_EL >= 1 && TM >= 1 && TN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM];
+  __shared__ float Bs[2][BK][BN];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int m0 = blockIdx.y * BM;
+  const long n0 = (long)blockIdx.x * BN;
+  const int kbeg = blockIdx.z * a.g.kper;
+  const int kend = min(a.g.K, kbeg + a.g.kper);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  // ---- per-thread pixel of the B operand
+  const int bn = tid % BN;
+  const int brow = __builtin_amdgcn_readfirstlane(tid / BN);
+  const long n = n0 + bn;
+  const bool nvalid = n < a.g.N;
+  int py = 0, px = 0;
+  const float* base0 = nullptr;
+  const float* base1 = nullptr;
+  if (nvalid) {
+    const int img = (int)fdiv((uint32_t)n, a.fd_pix);
+    const int pix = (int)(n - (long)img * a.fd_pix.d);
+    const int oy = (int)fdiv((uint32_t)pix, a.fd_row);
+    const int ox = pix - oy * (int)a.fd_row.d;
+    if (MODE == 0) {
+      py = oy * S - a.pad;
+      px = ox * S - a.pad;
+      const int q = (int)fdiv((uint32_t)img, a.fd_bdiv);
+      base0 = a.in.p0 + (long)(img - q * (int)a.fd_bdiv.d) * a.in.bs0 + (long)q * a.in.bhi;
+      base1 = a.in.p1 ? a.in.p1 + (long)img * a.in.bs1 : nullptr;
+    } else {
+      py = oy;   // dX pixel (ih, iw)
+      px = ox;
+      base0 = a.dy + (long)img * a.Cout * a.HoWo;
+    }
+  }
+
+  float4 areg[A_F4];
+  float breg[B_EL];
+
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < A_F4; ++j) {
+      const int idx = tid + 256 * j;
+      const int row = idx / (BM / 4), c4 = idx % (BM / 4);
+      if (A_TOT % 256 == 0 || idx < A_TOT)
+        areg[j] = *reinterpret_cast<const float4*>(a.A + (long)(k0 + row) * a.g.Mpad + m0 + c4 * 4);
+    }
+  };
+  auto load_b = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < B_EL; ++j) {
+      const int k = k0 + brow + j * B_RS;   // wave-uniform
+      float v = 0.f;
+      if (k < kend) {
+        const int c = k / KK;
+        const int r = k - c * KK;
+        const int kh = r / KW, kw = r - (r / KW) * KW;
+        if (MODE == 0) {
+          int iy = py + kh, ix = px + kw;
+          bool ok = nvalid;
+          if (RFL) {
+            iy = refl(iy, a.H);
+            ix = refl(ix, a.W);
+          } else {
+            ok = ok && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+          }
+          const float* src = (c < a.in.c0) ? base0 + (long)c * a.HW : base1 + (long)(c - a.in.c0) * a.HW;
+          if (ok) v = src[iy * a.W + ix];
+        } else {
+          const float* d = base0 + (long)c * a.HoWo;
+          if (!RFL) {
+            const int ohn = py + a.pad - kh, own = px + a.pad - kw;
+            if (S == 1) {
+              if (nvalid && (unsigned)ohn < (unsigned)a.Ho && (unsigned)own < (unsigned)a.Wo)
+                v = d[ohn * a.Wo + own];
+            } else {
+              if (nvalid && ohn >= 0 && own >= 0 && (ohn % S) == 0 && (own % S) == 0) {
+                const int oh = ohn / S, ow = own / S;
+                if (oh < a.Ho && ow < a.Wo) v = d[oh * a.Wo + ow];
+              }
+            }
+          } else if (nvalid) {
+            // pad_reflect adjoint: padded rows q with reflect(q-1) == iy are iy+1, 0 (iy == 1)
+            // and H+1 (iy == H-2); same for columns (stride 1, pad 1).
+            const int qy[3] = {py + 1, (py == 1) ? 0 : -1000, (py == a.H - 2) ? a.H + 1 : -1000};
+            const int qx[3] = {px + 1, (px == 1) ? 0 : -1000, (px == a.W - 2) ? a.W + 1 : -1000};
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+              const int oh = qy[u] - kh;
+              if ((unsigned)oh >= (unsigned)a.Ho) continue;
+#pragma unroll
+              for (int w = 0; w < 3; ++w) {
+                const int ow = qx[w] - kw;
+                if ((unsigned)ow >= (unsigned)a.Wo) continue;
+                v += d[oh * a.Wo + ow];
+              }
+            }
+          }
+        }
+      }
+      breg[j] = v;
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < A_F4; ++j) {
+      const int idx = tid + 256 * j;
+      const int row = idx / (BM / 4), c4 = idx % (BM / 4);
+      if (A_TOT % 256 == 0 || idx < A_TOT) *reinterpret_cast<float4*>(&As[buf][row][c4 * 4]) = areg[j];
+    }
+#pragma unroll
+    for (int j = 0; j < B_EL; ++j) Bs[buf][brow + j * B_RS][bn] = breg[j];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  load_a(kbeg);
+  load_b(kbeg);
+  store_tiles(0);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) {
+      load_a(kbeg + (t + 1) * BK);
+      load_b(kbeg + (t + 1) * BK);
+    }
+    mma_chunk<TM, TN, BK>(&As[cur][0][0], BM, &Bs[cur][0][0], BN, wm * TM * 32, wn * TN * 32, lane, acc);
+    if (t + 1 < nk) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const long nn = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+    if (nn >= a.g.N) continue;
+    if (a.slab) {
+      float* sl = a.slab + (long)blockIdx.z * a.g.M * a.g.N;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (m < a.g.M) sl[(long)m * a.g.N + nn] = acc[i][j][r];
+        }
+    } else {
+      const int img = (int)fdiv((uint32_t)nn, a.fd_pix);
+      const long pix = nn - (long)img * a.fd_pix.d;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (m < a.g.M) store_out(a.out, m, img, pix, a.fd_pix.d, acc[i][j][r]);
+        }
+    }
+  }
+}
+
+// split-K reduction + epilogue for fwd / dgrad
+__global__ __launch_bounds__(256) void splitk_reduce_px_kernel(ConvArgs a, int splits) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)a.g.M * a.g.N;
+  if (idx >= total) return;
+  const int m = (int)(idx / a.g.N);
+  const long nn = idx - (long)m * a.g.N;
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += a.slab[(long)s * total + idx];
+  const int img = (int)fdiv((uint32_t)nn, a.fd_pix);
+  const long pix = nn - (long)img * a.fd_pix.d;
+  store_out(a.out, m, img, pix, a.fd_pix.d, v);
+}
+
+// ---------------------------------------------------------------------------------------------
+// wgrad kernel: lanes along the pixel (K) axis for both operands, transposed into LDS
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, int BK, int WM, int WN, int KH, int KW, int S, int RFL>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
+  constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN);
+  constexpr int KK = KH * KW;
+  constexpr int RP = 256 / BK;          // rows per pass
+  constexpr int A_EL = BM / RP, B_EL = BN / RP;
+  constexpr int LDA = BM + 1, LDB = BN + 1;
+  static_assert(A_EL >= 1 && B_EL >= 1, "tile");
+  __shared__ float As[2][BK][LDA];
+  __shared__ float Bs[2][BK][LDB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int m0 = blockIdx.y * BM;
+  const int n0 = blockIdx.x * BN;
+  const long kbeg = (long)blockIdx.z * a.g.kper;
+  const long Ktot = a.g.K;
+  const long kend = min(Ktot, kbeg + (long)a.g.kper);
+  const int nk = (int)((kend - kbeg + BK - 1) / BK);
+  const int kl = tid % BK;
+  const int rg = tid / BK;
+
+  // per-thread filter columns of B (fixed for the whole kernel)
+  float areg[A_EL], breg[B_EL];
+
+  auto load = [&](long k0) {
+    const long p = k0 + kl;
+    const bool pv = p < kend;
+    int img = 0, oy = 0, ox = 0;
+    if (pv) {
+      img = (int)fdiv((uint32_t)p, a.fd_pix);
+      const int pix = (int)(p - (long)img * a.fd_pix.d);
+      oy = (int)fdiv((uint32_t)pix, a.fd_row);
+      ox = pix - oy * (int)a.fd_row.d;
+    }
+    const float* dyb = a.dy + (long)img * a.Cout * a.HoWo + (long)oy * a.Wo + ox;
+#pragma unroll
+    for (int j = 0; j < A_EL; ++j) {
+      const int m = m0 + rg + j * RP;
+      areg[j] = (pv && m < a.g.M) ? dyb[(long)m * a.HoWo] : 0.f;
+    }
+    const int q = (int)fdiv((uint32_t)img, a.fd_bdiv);
+    const float* b0 = a.in.p0 + (long)(img - q * (int)a.fd_bdiv.d) * a.in.bs0 + (long)q * a.in.bhi;
+    const float* b1 = a.in.p1 ? a.in.p1 + (long)img * a.in.bs1 : nullptr;
+    const int py = oy * S - a.pad, px = ox * S - a.pad;
+#pragma unroll
+    for (int j = 0; j < B_EL; ++j) {
+      const int nidx = n0 + rg + j * RP;
+      float v = 0.f;
+      if (pv && nidx < a.g.N) {
+        const int c = nidx / KK;
+        const int r = nidx - c * KK;
+        const int kh = r / KW, kw = r - (r / KW) * KW;
+        int iy = py + kh, ix = px + kw;
+        bool ok = true;
+        if (RFL) {
+          iy = refl(iy, a.H);
+          ix = refl(ix, a.W);
+        } else {
+          ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+        }
+        const float* src = (c < a.in.c0) ? b0 + (long)c * a.HW : b1 + (long)(c - a.in.c0) * a.HW;
+        if (ok) v = src[iy * a.W + ix];
+      }
+      breg[j] = v;
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < A_EL; ++j) As[buf][kl][rg + j * RP] = areg[j];
+#pragma unroll
+    for (int j = 0; j < B_EL; ++j) Bs[buf][kl][rg + j * RP] = breg[j];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) {
+    load(kbeg);
+    store_tiles(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) load(kbeg + (long)(t + 1) * BK);
+    mma_chunk<TM, TN, BK>(&As[cur][0][0], LDA, &Bs[cur][0][0], LDB, wm * TM * 32, wn * TN * 32, lane, acc);
+    if (t + 1 < nk) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  float* sl = a.slab + (long)blockIdx.z * a.g.M * a.g.N;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const long nn = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+    if (nn >= a.g.N) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < a.g.M) sl[(long)m * a.g.N + nn] = acc[i][j][r];
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_w_kernel(const float* __restrict__ slab,
+                                                              int splits, long total,
+                                                              float* __restrict__ dw, int acc) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += slab[(long)s * total + idx];
+  if (acc)
+    dw[idx] += v;
+  else
+    dw[idx] = v;
+}
+
+// bias gradient: db[c] = sum over images and pixels of dY[img][c][:]  (one block per channel)
+__global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict__ dy, int N,
+                                                        int C, long HW, float* __restrict__ db,
+                                                        int acc) {
+  __shared__ float red[4];
+  const int c = blockIdx.x;
+  float s = 0.f;
+  for (int img = 0; img < N; ++img) {
+    const float* p = dy + ((long)img * C + c) * HW;
+    for (long i = threadIdx.x; i < HW; i += 256) s += p[i];
+  }
+  float v[1] = {s};
+  block_sum256<1>(v, red);
+  if (threadIdx.x == 0) {
+    if (acc)
+      db[c] += v[0];
+    else
+      db[c] = v[0];
+  }
+}
+
+__global__ __launch_bounds__(256) void act_backward_kernel(const float* __restrict__ out,
+                                                           const float* __restrict__ dout,
+                                                           float* __restrict__ dpre, long n,
+                                                           int act) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float o = out[i], g = dout[i];
+  float d;
+  switch (act) {
+    case ACT_RELU: d = o > 0.f ? g : 0.f; break;
+    case ACT_ELU: d = o > 0.f ? g : g * (o + 1.f); break;      // elu'(x) = exp(x) = out + 1
+    case ACT_SIGMOID: d = g * o * (1.f - o); break;
+    default: d = g;
+  }
+  dpre[i] = d;
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side: tile selection, split-K planning, dispatch
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int TARGET_BLOCKS = 768;   // ~3 blocks per CU on 256 CUs
+
+enum TileCfg { T128x128 = 0, T64x256 = 1, T32x256 = 2 };
+
+struct Plan {
+  int tile;
+  int BM, BN, BK;
+  int splits;
+  int kper;
+};
+
+Plan plan_px(int M, long N, int K) {
+  Plan p{};
+  if (M > 64) {
+    p.tile = T128x128; p.BM = 128; p.BN = 128;
+  } else if (M > 32) {
+    p.tile = T64x256; p.BM = 64; p.BN = 256;
+  } else {
+    p.tile = T32x256; p.BM = 32; p.BN = 256;
+  }
+  p.BK = 16;
+  const long tiles = (long)cdiv(M, p.BM) * cdiv(N, p.BN);
+  int splits = 1;
+  while (tiles * splits * 2 <= TARGET_BLOCKS && K / (splits * 2) >= 8 * p.BK) splits *= 2;
+  p.kper = (int)round_up(cdiv(K, splits), p.BK);
+  p.splits = cdiv(K, p.kper);
+  return p;
+}
+
+Plan plan_w(int M, long N, long K) {
+  Plan p{};
+  p.BM = 64; p.BN = 128; p.BK = 32;
+  const long tiles = (long)cdiv(M, p.BM) * cdiv(N, p.BN);
+  long splits = std::max(1L, (long)TARGET_BLOCKS / tiles);
+  splits = std::min(splits, std::max(1L, K / (8 * p.BK)));
+  p.kper = (int)round_up((K + splits - 1) / splits, p.BK);
+  p.splits = (int)((K + p.kper - 1) / p.kper);
+  return p;
+}
+
+void fill_common(ConvArgs& a, const ConvShape& s) {
+  a.Cin = s.Cin; a.H = s.H; a.W = s.W; a.Cout = s.Cout; a.Ho = s.Ho; a.Wo = s.Wo;
+  a.stride = s.stride; a.pad = s.pad;
+  a.HW = (long)s.H * s.W;
+  a.HoWo = (long)s.Ho * s.Wo;
+}
+
+int check_shape(const ConvShape& s) {
+  MD2_CHECK_ARG(s.N > 0 && s.Cin > 0 && s.Cout > 0 && s.H > 0 && s.W > 0, "conv dims");
+  MD2_CHECK_ARG(s.KH == s.KW && (s.KH == 1 || s.KH == 3 || s.KH == 7), "kernel size 1/3/7");
+  MD2_CHECK_ARG(s.stride == 1 || s.stride == 2, "stride 1/2");
+  MD2_CHECK_ARG(s.Ho == (s.H + 2 * s.pad - s.KH) / s.stride + 1 &&
+                    s.Wo == (s.W + 2 * s.pad - s.KW) / s.stride + 1, "output size");
+  MD2_CHECK_ARG(!s.reflect || (s.KH == 3 && s.stride == 1 && s.pad == 1 && s.H >= 2 && s.W >= 2),
+                "reflect padding needs 3x3/1 pad 1");
+  MD2_CHECK_ARG((long)s.N * s.H * s.W < (1L << 31) && (long)s.N * s.Ho * s.Wo < (1L << 31),
+                "pixel count");
+  return MD2_OK;
+}
+
+// (KH, S, RFL) combos instantiated
+#define MD2_CONV_COMBOS(X) X(1, 1, 0) X(1, 2, 0) X(3, 1, 0) X(3, 1, 1) X(3, 2, 0) X(7, 2, 0)
+
+template <int MODE, int BM, int BN, int WM, int WN>
+int launch_px_tile(const ConvShape& s, const ConvArgs& a, dim3 grid, hipStream_t st) {
+#define MD2_PX_CASE(KS, SS, RR)                                                                  \
+  if (s.KH == KS && s.stride == SS && s.reflect == RR) {                                         \
+    hipLaunchKernelGGL((conv_px_kernel<MODE, BM, BN, 16, WM, WN, KS, KS, SS, RR>), grid, dim3(256), \
+                       0, st, a);                                                                \
+    MD2_LAUNCH_CHECK();                                                                          \
+    return MD2_OK;                                                                               \
+  }
+  MD2_CONV_COMBOS(MD2_PX_CASE)
+#undef MD2_PX_CASE
+  set_error("conv: unsupported (kernel, stride, padding) combination");
+  return MD2_ENOTSUP;
+}
+
+template <int MODE>
+int launch_px(const ConvShape& s, ConvArgs& a, const Plan& p, ConvWorkspace ws, hipStream_t st) {
+  a.g.kper = p.kper;
+  a.slab = nullptr;
+  if (p.splits > 1) {
+    const size_t need = (size_t)p.splits * a.g.M * a.g.N * sizeof(float);
+    MD2_CHECK_ARG(ws.ptr && ws.bytes >= need, "conv split-K workspace too small");
+    a.slab = (float*)ws.ptr;
+  }
+  dim3 grid(cdiv(a.g.N, p.BN), cdiv(a.g.M, p.BM), p.splits);
+  int rc;
+  switch (p.tile) {
+    case T128x128: rc = launch_px_tile<MODE, 128, 128, 2, 2>(s, a, grid, st); break;
+    case T64x256: rc = launch_px_tile<MODE, 64, 256, 1, 4>(s, a, grid, st); break;
+    default: rc = launch_px_tile<MODE, 32, 256, 1, 4>(s, a, grid, st); break;
+  }
+  if (rc) return rc;
+  if (p.splits > 1) {
+    const long total = (long)a.g.M * a.g.N;
+    hipLaunchKernelGGL(splitk_reduce_px_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a, p.splits);
+    MD2_LAUNCH_CHECK();
+  }
+  return MD2_OK;
+}
+
+}  // namespace
+
+size_t conv_fwd_workspace(const ConvShape& s) {
+  const long N = (long)s.N * s.Ho * s.Wo;
+  const Plan p = plan_px(s.Cout, N, s.Cin * s.KH * s.KW);
+  return p.splits > 1 ? (size_t)p.splits * s.Cout * N * sizeof(float) : 0;
+}
+
+size_t conv_dgrad_workspace(const ConvShape& s) {
+  const long N = (long)s.N * s.H * s.W;
+  const Plan p = plan_px(s.Cin, N, s.Cout * s.KH * s.KW);
+  return p.splits > 1 ? (size_t)p.splits * s.Cin * N * sizeof(float) : 0;
+}
+
+size_t conv_wgrad_workspace(const ConvShape& s) {
+  const long K = (long)s.N * s.Ho * s.Wo;
+  const long Nc = (long)s.Cin * s.KH * s.KW;
+  const Plan p = plan_w(s.Cout, Nc, K);
+  return (size_t)p.splits * s.Cout * Nc * sizeof(float);
+}
+
+int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const TensorOut& y,
+             ConvWorkspace ws, hipStream_t st) {
+  MD2_TRY(check_shape(s));
+  MD2_CHECK_ARG(x.p0 && wpacked && y.p0, "conv_fwd pointers");
+  MD2_CHECK_ARG(x.c0 == s.Cin || x.p1 != nullptr, "conv_fwd: second input tensor missing");
+  ConvArgs a{};
+  fill_common(a, s);
+  a.g.M = s.Cout;
+  a.g.N = (long)s.N * s.Ho * s.Wo;
+  a.g.K = s.Cin * s.KH * s.KW;
+  a.g.Mpad = (int)round_up(s.Cout, MPAD);
+  a.fd_pix = make_fastdiv((uint32_t)(s.Ho * s.Wo));
+  a.fd_row = make_fastdiv((uint32_t)s.Wo);
+  a.fd_bdiv = make_fastdiv((uint32_t)std::min(x.bdiv, 1 << 30));
+  a.in = x;
+  a.A = wpacked;
+  a.out = y;
+  const Plan p = plan_px(a.g.M, a.g.N, a.g.K);
+  return launch_px<0>(s, a, p, ws, st);
+}
+
+int conv_dgrad(const ConvShape& s, const float* dy, const float* wpacked_d, const TensorOut& dx,
+               ConvWorkspace ws, hipStream_t st) {
+  MD2_TRY(check_shape(s));
+  MD2_CHECK_ARG(dy && wpacked_d && dx.p0, "conv_dgrad pointers");
+  MD2_CHECK_ARG(!dx.bias && dx.act == ACT_NONE, "conv_dgrad: no bias/activation on dX");
+  ConvArgs a{};
+  fill_common(a, s);
+  a.g.M = s.Cin;
+  a.g.N = (long)s.N * s.H * s.W;
+  a.g.K = s.Cout * s.KH * s.KW;
+  a.g.Mpad = (int)round_up(s.Cin, MPAD);
+  a.fd_pix = make_fastdiv((uint32_t)(s.H * s.W));
+  a.fd_row = make_fastdiv((uint32_t)s.W);
+  a.fd_bdiv = make_fastdiv(1u << 30);
+  a.dy = dy;
+  a.A = wpacked_d;
+  a.out = dx;
+  const Plan p = plan_px(a.g.M, a.g.N, a.g.K);
+  return launch_px<1>(s, a, p, ws, st);
+}
+
+int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw, float* db,
+               int accumulate, ConvWorkspace ws, hipStream_t st) {
+  MD2_TRY(check_shape(s));
+  MD2_CHECK_ARG(x.p0 && dy && dw, "conv_wgrad pointers");
+  ConvArgs a{};
+  fill_common(a, s);
+  const long Kpix = (long)s.N * s.Ho * s.Wo;
+  a.g.M = s.Cout;
+  a.g.N = (long)s.Cin * s.KH * s.KW;
+  a.g.K = (int)Kpix;
+  a.fd_pix = make_fastdiv((uint32_t)(s.Ho * s.Wo));
+  a.fd_row = make_fastdiv((uint32_t)s.Wo);
+  a.fd_bdiv = make_fastdiv((uint32_t)std::min(x.bdiv, 1 << 30));
+  a.in = x;
+  a.dy = dy;
+  const Plan p = plan_w(a.g.M, a.g.N, Kpix);
+  a.g.kper = p.kper;
+  const size_t need = (size_t)p.splits * a.g.M * a.g.N * sizeof(float);
+  MD2_CHECK_ARG(ws.ptr && ws.bytes >= need, "conv_wgrad workspace too small");
+  a.slab = (float*)ws.ptr;
+  dim3 grid(cdiv(a.g.N, p.BN), cdiv(a.g.M, p.BM), p.splits);
+  bool launched = false;
+#define MD2_W_CASE(KS, SS, RR)                                                                     \
+  if (!launched && s.KH == KS && s.stride == SS && s.reflect == RR) {                              \
+    hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 32, 2, 2, KS, KS, SS, RR>), grid, dim3(256), 0, \
+                       st, a);                                                                     \
+    launched = true;                                                                               \
+  }
+  MD2_CONV_COMBOS(MD2_W_CASE)
+#undef MD2_W_CASE
+  if (!launched) {
+    set_error("conv_wgrad: unsupported (kernel, stride, padding) combination");
+    return MD2_ENOTSUP;
+  }
+  MD2_LAUNCH_CHECK();
+  const long total = (long)a.g.M * a.g.N;
+  hipLaunchKernelGGL(splitk_reduce_w_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a.slab,
+                     p.splits, total, dw, accumulate);
+  MD2_LAUNCH_CHECK();
+  if (db) {
+    hipLaunchKernelGGL(bias_grad_kernel, dim3(s.Cout), dim3(256), 0, st, dy, s.N, s.Cout,
+                       (long)s.Ho * s.Wo, db, accumulate);
+    MD2_LAUNCH_CHECK();
+  }
+  return MD2_OK;
+}
+
+int act_backward(const float* out, const float* dout, float* dpre, long n, int act,
+                 hipStream_t st) {
+  hipLaunchKernelGGL(act_backward_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, out, dout, dpre, n,
+                     act);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+}  // namespace md2

@@ -38,6 +38,12 @@ class LossOut(C.Structure):
     ]
 
 
+class ConvDesc(C.Structure):
+    """``md2_conv_desc``."""
+    _fields_ = [(n, C.c_int) for n in ("n", "cin", "h", "w", "cout", "kh", "kw", "stride", "pad",
+                                       "reflect", "act")]
+
+
 _lib = None
 _load_error = None
 
@@ -52,6 +58,11 @@ _SIGS = {
     "md2_loss_fwd_bwd": (C.c_int, [C.POINTER(LossCfg), FP, P, P, P, C.c_float, C.POINTER(LossOut), P, P]),
     "md2_so3_compose_fwd": (C.c_int, [P, C.c_int, C.c_int, P, P]),
     "md2_so3_compose_bwd": (C.c_int, [P, C.c_int, C.c_int, P, P, P]),
+    "md2_conv2d_workspace_size": (C.c_size_t, [C.POINTER(ConvDesc)]),
+    "md2_conv2d_fwd": (C.c_int, [C.POINTER(ConvDesc), P, P, P, P, P, P]),
+    "md2_conv2d_dgrad": (C.c_int, [C.POINTER(ConvDesc), P, P, P, P, P]),
+    "md2_conv2d_wgrad": (C.c_int, [C.POINTER(ConvDesc), P, P, P, P, P, P]),
+    "md2_act_backward": (C.c_int, [P, P, P, C.c_longlong, C.c_int, P]),
 }
 
 

@@ -1,0 +1,84 @@
+"""GPU parity of the implicit-GEMM conv kernels (fwd / ∇conv_data / ∇conv_filter) against
+fp64 torch-CPU convolutions (the oracle's F.conv2d, cross-correlation semantics).
+
+Tolerance: relative Frobenius error 1e-5 (exact-fp32 MFMA accumulation over K <= 8k terms)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import md2_oracle as O
+from tests import _data as D
+
+pytestmark = pytest.mark.gpu
+
+# (x_shape, cout, k, stride, pad, reflect, act, bias)   -- shapes of the ResNet-18 / decoders
+CASES = [
+    ((2, 3, 64, 208), 64, 7, 2, 3, False, None, False),          # stem 7x7/2
+    ((2, 64, 32, 104), 64, 3, 1, 1, False, None, False),         # layer1
+    ((2, 64, 32, 104), 128, 3, 2, 1, False, None, False),        # layer2.0.conv1 (stride 2)
+    ((2, 64, 32, 104), 128, 1, 2, 0, False, None, False),        # downsample 1x1/2
+    ((2, 256, 8, 26), 512, 3, 2, 1, False, None, False),         # layer4.0.conv1 (split-K)
+    ((3, 512, 4, 13), 512, 3, 1, 1, False, None, False),         # layer4 3x3 (split-K)
+    ((2, 96, 16, 52), 32, 3, 1, 1, True, "elu", True),           # decoder c2 (reflect, ELU)
+    ((2, 16, 32, 64), 16, 3, 1, 1, True, "elu", True),           # decoder branch5
+    ((2, 16, 32, 64), 1, 3, 1, 1, True, "sigmoid", True),        # disparity head
+    ((4, 512, 4, 13), 256, 3, 1, 1, False, "relu", True),        # pose conv1
+    ((4, 256, 4, 13), 6, 1, 1, 0, False, None, True),            # pose conv3
+    ((6, 512, 4, 13), 256, 1, 1, 0, False, "relu", True),        # pose squeezer
+    ((2, 8, 2, 3), 4, 3, 1, 1, True, "elu", True),               # reflect on a 2x3 map
+    ((3, 5, 9, 11), 7, 3, 2, 1, False, "relu", True),            # ragged everything
+]
+
+
+def _ref_act(y, act):
+    return {None: y, "relu": F.relu(y), "elu": F.elu(y), "sigmoid": torch.sigmoid(y)}[act]
+
+
+def _ref_conv(x, w, b, stride, pad, reflect):
+    if reflect:
+        return F.conv2d(O.pad_reflect(x, pad), w, b, stride=stride)
+    return F.conv2d(x, w, b, stride=stride, padding=pad)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-{c[1]}-k{c[2]}s{c[3]}{'r' if c[5] else ''}" for c in CASES])
+def test_conv_fwd_bwd(case):
+    from md2hip import ops
+    xs, cout, k, stride, pad, reflect, act, has_bias = case
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(*xs, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, xs[1], k, k, generator=g, dtype=torch.float64) / (xs[1] * k * k) ** 0.5
+    b = torch.randn(cout, generator=g, dtype=torch.float64) if has_bias else None
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True) if has_bias else None
+    pre = _ref_conv(xr, wr, br, stride, pad, reflect)
+    y_ref = _ref_act(pre, act)
+    dy = torch.randn(pre.shape, generator=g, dtype=torch.float64)
+    pre.backward(dy)
+
+    dev = torch.device("cuda")
+    xg, wg = x.float().to(dev), w.float().to(dev)
+    bg = b.float().to(dev) if has_bias else None
+    y = ops.conv2d(xg, wg, bg, stride=stride, pad=pad, reflect=reflect, act=act)
+    dx = ops.conv2d_dgrad(dy.float().to(dev), wg, xs, stride=stride, pad=pad, reflect=reflect)
+    dw, db = ops.conv2d_wgrad(xg, dy.float().to(dev), tuple(w.shape), stride=stride, pad=pad,
+                              reflect=reflect, bias=has_bias)
+    torch.cuda.synchronize()
+    assert D.rel_err(y, y_ref.detach()) < 1e-5
+    assert D.rel_err(dx, xr.grad) < 1e-5
+    assert D.rel_err(dw, wr.grad) < 1e-5
+    if has_bias:
+        assert D.rel_err(db, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("act", ["relu", "elu", "sigmoid"])
+def test_act_backward(act):
+    from md2hip import ops
+    g = torch.Generator().manual_seed(9)
+    pre = torch.randn(1000, generator=g, dtype=torch.float64).requires_grad_(True)
+    out = _ref_act(pre, act)
+    dout = torch.randn(1000, generator=g, dtype=torch.float64)
+    out.backward(dout)
+    got = ops.act_backward(out.detach().float().cuda(), dout.float().cuda(), act)
+    torch.cuda.synchronize()
+    assert D.rel_err(got, pre.grad) < 1e-5
