@@ -41,6 +41,8 @@ int md2_abi_version(void);
 const char* md2_last_error(void);
 /* number of visible HIP devices (host call; does not initialise a context). */
 int md2_device_count(int* count);
+/* async device-to-device copy on `stream` (used to hand library-owned outputs to the host) */
+int md2_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Loss tail: src/training.jl:25-77 (given the model's disparities and poses) -- forward value
@@ -115,6 +117,61 @@ int md2_conv2d_wgrad(const md2_conv_desc* d, const float* x, const float* dy, fl
 /* dpre = dout .* act'(out) from the stored post-activation output (n elements). */
 int md2_act_backward(const float* out, const float* dout, float* dpre, long long n, int act,
                      void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Model: Model(ResidualNetwork(arch), DepthDecoder(embedding_levels=0), PoseDecoder) in mono
+ * mode (src/model.jl:24-70), train_loss (src/training.jl:21-78), its pullback, Flux ADAM.
+ * Parameters / gradients are CALLER-owned flat fp32 device vectors; their order is the table
+ * of md2_arch_param_info (conv weights cross-correlation [cout][cin][kh][kw], then bias;
+ * BatchNorm gamma, beta).  x is [batch][3][c][h][w] (Julia (W,H,C,3,N)).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct md2_model_cfg {
+  int arch;                             /* ResidualNetwork depth: 18, 34 or 50              */
+  int in_channels;                      /* 1 (grayscale) or 3                                */
+  int batch;                            /* samples per step (triplets)                       */
+  int width, height;                    /* Params.target_size (multiples of 32)              */
+  int n_levels;                         /* length(scale_levels)                              */
+  int scale_levels[MD2_MAX_SCALES];     /* DepthDecoder scale_levels, increasing, last == 5  */
+  float K[9], invK[9];                  /* TrainCache.K / invK, row-major                    */
+  float min_depth, max_depth, disparity_smoothness;   /* Params                              */
+  float scales[MD2_MAX_SCALES];         /* TrainCache.scales                                 */
+  int automasking;                      /* Params.automasking                                */
+  int target, src0, src1;               /* 0-based frame ids (only 1, 0, 2 supported)        */
+} md2_model_cfg;
+
+typedef struct md2_model md2_model;
+
+/* host-only queries of the flat parameter table (no device needed) */
+int md2_arch_param_count(const md2_model_cfg* cfg, long long* n_entries, long long* n_elems);
+int md2_arch_param_info(const md2_model_cfg* cfg, int idx, char* name, int name_len, int* ndim,
+                        int* shape4, long long* offset);
+
+int md2_model_create(const md2_model_cfg* cfg, float* params, float* grads, md2_model** out);
+int md2_model_destroy(md2_model* m);
+size_t md2_model_device_bytes(md2_model* m);
+/* re-pack conv weights after the caller changed `params` directly */
+int md2_model_repack(md2_model* m, void* stream);
+/* forward (encoder on 3*batch frames, decoder on targets, poses) + train_loss value + the
+ * loss-tail pullback; terms: [n_levels][2] or NULL */
+int md2_model_forward_loss(md2_model* m, const float* x, const float* auto_loss, float* loss,
+                           float* terms, void* stream);
+/* backward in segments (0 = pose+depth decoders, 1..4 = layer4..layer1, 5 = stem); after
+ * segment k the flat gradient range [off, off+len) is final (bucket for the DP all-reduce) */
+int md2_model_num_segments(md2_model* m);
+int md2_model_backward_segment(md2_model* m, int k, long long* off, long long* len,
+                               void* stream);
+/* Flux ADAM step over the flat vectors (bias correction with `step` >= 1); gradients are
+ * multiplied by grad_scale first (1/world_size after a sum all-reduce); re-packs weights */
+int md2_model_adam(md2_model* m, float* adam_m, float* adam_v, float lr, float beta1,
+                   float beta2, float eps, int step, float grad_scale, void* stream);
+/* forward_loss + every backward segment + ADAM (single-GPU step) */
+int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, float* adam_m,
+                         float* adam_v, float lr, int step, float* loss, void* stream);
+/* device pointers of the last forward: disparities per level and poses [2*batch][6] */
+int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose);
+/* eval_disparity (src/model.jl:63) on x [n][c][h][w], n <= batch; disp: per-level pointers */
+int md2_model_eval_disparity(md2_model* m, const float* x, int n, const float** disp,
+                             void* stream);
 
 #ifdef __cplusplus
 }

@@ -6,6 +6,7 @@
 
 #include "conv.h"
 #include "loss_tail.h"
+#include "model.h"
 
 #include <algorithm>
 
@@ -54,6 +55,12 @@ const char* md2_last_error(void) { return md2::last_error(); }
 int md2_device_count(int* count) {
   MD2_CHECK_ARG(count != nullptr, "count");
   MD2_HIP(hipGetDeviceCount(count));
+  return MD2_OK;
+}
+
+int md2_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
+  MD2_CHECK_ARG(dst && src, "memcpy pointers");
+  MD2_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return MD2_OK;
 }
 
@@ -168,6 +175,135 @@ int md2_act_backward(const float* out, const float* dout, float* dpre, long long
                      void* stream) {
   MD2_CHECK_ARG(out && dout && dpre && n >= 0, "act_backward args");
   return act_backward(out, dout, dpre, (long)n, act, (hipStream_t)stream);
+}
+
+// ---- model -----------------------------------------------------------------------------------
+static ArchCfg to_arch(const md2_model_cfg* c) {
+  ArchCfg a;
+  a.arch = c->arch;
+  a.in_ch = c->in_channels;
+  a.nlevels = c->n_levels;
+  for (int i = 0; i < MAX_SCALES; ++i) a.levels[i] = c->scale_levels[i];
+  return a;
+}
+
+int md2_arch_param_count(const md2_model_cfg* cfg, long long* n_entries, long long* n_elems) {
+  MD2_CHECK_ARG(cfg != nullptr, "cfg");
+  MD2_CHECK_ARG(cfg->arch == 18 || cfg->arch == 34 || cfg->arch == 50, "arch 18/34/50");
+  MD2_CHECK_ARG(cfg->n_levels >= 1 && cfg->n_levels <= 4, "n_levels");
+  const auto t = build_param_table(to_arch(cfg));
+  if (n_entries) *n_entries = (long long)t.size();
+  if (n_elems) *n_elems = t.empty() ? 0 : (long long)(t.back().offset + t.back().numel);
+  return MD2_OK;
+}
+
+int md2_arch_param_info(const md2_model_cfg* cfg, int idx, char* name, int name_len, int* ndim,
+                        int* shape4, long long* offset) {
+  MD2_CHECK_ARG(cfg != nullptr, "cfg");
+  const auto t = build_param_table(to_arch(cfg));
+  MD2_CHECK_ARG(idx >= 0 && idx < (int)t.size(), "param index");
+  const ParamEntry& e = t[idx];
+  if (name && name_len > 0) {
+    std::strncpy(name, e.name.c_str(), name_len - 1);
+    name[name_len - 1] = 0;
+  }
+  if (ndim) *ndim = e.ndim;
+  if (shape4)
+    for (int i = 0; i < 4; ++i) shape4[i] = e.shape[i];
+  if (offset) *offset = e.offset;
+  return MD2_OK;
+}
+
+struct md2_model {
+  Model* impl;
+};
+
+int md2_model_create(const md2_model_cfg* c, float* params, float* grads, md2_model** out) {
+  MD2_CHECK_ARG(c && params && grads && out, "model_create args");
+  ModelCfg mc;
+  mc.arch = to_arch(c);
+  mc.N = c->batch;
+  mc.W = c->width;
+  mc.H = c->height;
+  std::memcpy(mc.K, c->K, sizeof(mc.K));
+  std::memcpy(mc.invK, c->invK, sizeof(mc.invK));
+  mc.min_depth = c->min_depth;
+  mc.max_depth = c->max_depth;
+  mc.smoothness = c->disparity_smoothness;
+  for (int i = 0; i < MAX_SCALES; ++i) mc.scales[i] = c->scales[i];
+  mc.automask = c->automasking;
+  mc.target = c->target;
+  mc.src0 = c->src0;
+  mc.src1 = c->src1;
+  Model* m = nullptr;
+  MD2_TRY(model_create(mc, params, grads, &m));
+  *out = new md2_model{m};
+  return MD2_OK;
+}
+
+int md2_model_destroy(md2_model* m) {
+  if (m) {
+    model_destroy(m->impl);
+    delete m;
+  }
+  return MD2_OK;
+}
+
+size_t md2_model_device_bytes(md2_model* m) { return m ? model_device_bytes(m->impl) : 0; }
+
+int md2_model_repack(md2_model* m, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_repack(m->impl, (hipStream_t)stream);
+}
+
+int md2_model_forward_loss(md2_model* m, const float* x, const float* auto_loss, float* loss,
+                           float* terms, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_forward_loss(m->impl, x, auto_loss, loss, terms, (hipStream_t)stream);
+}
+
+int md2_model_num_segments(md2_model* m) { return m ? model_num_segments(m->impl) : 0; }
+
+int md2_model_backward_segment(md2_model* m, int k, long long* off, long long* len,
+                               void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  long o = 0, l = 0;
+  MD2_TRY(model_backward_segment(m->impl, k, &o, &l, (hipStream_t)stream));
+  if (off) *off = o;
+  if (len) *len = l;
+  return MD2_OK;
+}
+
+int md2_model_adam(md2_model* m, float* adam_m, float* adam_v, float lr, float beta1,
+                   float beta2, float eps, int step, float grad_scale, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_adam(m->impl, adam_m, adam_v, lr, beta1, beta2, eps, step, grad_scale,
+                    (hipStream_t)stream);
+}
+
+int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, float* adam_m,
+                         float* adam_v, float lr, int step, float* loss, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  hipStream_t st = (hipStream_t)stream;
+  MD2_TRY(model_forward_loss(m->impl, x, auto_loss, loss, nullptr, st));
+  for (int k = 0; k < model_num_segments(m->impl); ++k)
+    MD2_TRY(model_backward_segment(m->impl, k, nullptr, nullptr, st));
+  return model_adam(m->impl, adam_m, adam_v, lr, 0.9f, 0.999f, 1e-8f, step, 1.f, st);
+}
+
+int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose) {
+  MD2_CHECK_ARG(m, "model");
+  return model_outputs(m->impl, disp, w, h, pose);
+}
+
+int md2_model_eval_disparity(md2_model* m, const float* x, int n, const float** disp,
+                             void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  float* d[MAX_SCALES] = {};
+  MD2_TRY(model_eval_disparity(m->impl, x, n, d, (hipStream_t)stream));
+  if (disp)
+    for (int i = 0; i < MAX_SCALES; ++i) disp[i] = d[i];
+  return MD2_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,912 @@
+// Model executor (see model.h).
+//
+// Data layout in HBM (all fp32, NCHW == Julia (W,H,C,N)):
+//   * encoder batch is FRAME-MAJOR: image b = l*N + n holds frame l of sample n (the stem reads
+//     x[n][l] through a batch map), so the target frames form the contiguous slice [N, 2N) that
+//     the DepthDecoder reads as skips, and pose pairs (frame s, frame s+1) are (b, b+N).  BatchNorm
+//     statistics run over all 3N frames exactly like ResNet.jl on reshape(x, (W,H,C,L*N)).
+//   * parameters / gradients are caller-owned flat fp32 vectors in the order of
+//     oracle/md2_oracle.py param_spec; conv weights are re-packed K-major after each update.
+#include "model.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace md2 {
+
+namespace {
+
+struct PConv {
+  int cin = 0, cout = 0, k = 1, stride = 1, pad = 0, reflect = 0;
+  bool bias = false;
+  long w = -1, b = -1;
+};
+struct PBN {
+  int c = 0;
+  long g = -1, b = -1;
+};
+struct BlockSpec {
+  std::vector<PConv> convs;
+  std::vector<PBN> bns;
+  bool down = false;
+  PConv dconv;
+  PBN dbn;
+  int cin = 0, cout = 0, stride = 1;
+};
+struct BranchSpec {
+  int bid = 0;
+  PConv c1, c2;
+  int cin = 0, cout = 0, cskip = 0;
+  int head = -1;          // index into heads when a DecoderBlock head follows this branch
+};
+struct ArchSpec {
+  std::vector<ParamEntry> table;
+  long total = 0;
+  PConv stem;
+  PBN stem_bn;
+  std::vector<std::vector<BlockSpec>> stages;
+  int enc_ch[5];
+  std::vector<BranchSpec> branches;
+  std::vector<PConv> heads;
+  std::vector<int> head_level;
+  PConv squeezer, p1, p2, p3;
+  long stage_begin[5];    // flat offsets: [0] stem, [1..4] layer1..4
+  long depth_begin = 0;
+};
+
+ArchSpec build_spec(const ArchCfg& a) {
+  ArchSpec S;
+  auto add = [&](const std::string& name, std::initializer_list<int> shape) -> long {
+    ParamEntry e;
+    e.name = name;
+    e.ndim = (int)shape.size();
+    long n = 1;
+    int i = 0;
+    for (int s : shape) {
+      e.shape[i++] = s;
+      n *= s;
+    }
+    for (; i < 4; ++i) e.shape[i] = 1;
+    e.offset = S.total;
+    e.numel = n;
+    S.total += n;
+    S.table.push_back(e);
+    return e.offset;
+  };
+  auto conv = [&](const std::string& name, int cin, int cout, int k, int stride, int pad,
+                  int reflect, bool bias) {
+    PConv c;
+    c.cin = cin; c.cout = cout; c.k = k; c.stride = stride; c.pad = pad; c.reflect = reflect;
+    c.bias = bias;
+    c.w = add(name + ".weight", {cout, cin, k, k});
+    if (bias) c.b = add(name + ".bias", {cout});
+    return c;
+  };
+  auto bn = [&](const std::string& name, int c) {
+    PBN b;
+    b.c = c;
+    b.g = add(name + ".gamma", {c});
+    b.b = add(name + ".beta", {c});
+    return b;
+  };
+  const bool bottleneck = a.arch >= 50;
+  const int* layers;
+  static const int L18[4] = {2, 2, 2, 2}, L34[4] = {3, 4, 6, 3};
+  layers = (a.arch == 18) ? L18 : L34;
+  const int exp = bottleneck ? 4 : 1;
+  S.stage_begin[0] = 0;
+  S.stem = conv("encoder.stem.conv", a.in_ch, 64, 7, 2, 3, 0, false);
+  S.stem_bn = bn("encoder.stem.bn", 64);
+  int cin = 64;
+  const int widths[4] = {64, 128, 256, 512};
+  S.stages.resize(4);
+  for (int si = 0; si < 4; ++si) {
+    S.stage_begin[si + 1] = S.total;
+    for (int bi = 0; bi < layers[si]; ++bi) {
+      const int stride = (bi == 0 && si > 0) ? 2 : 1;
+      const std::string p = "encoder.layer" + std::to_string(si + 1) + "." + std::to_string(bi);
+      const int width = widths[si], cout = width * exp;
+      BlockSpec B;
+      B.cin = cin;
+      B.cout = cout;
+      B.stride = stride;
+      if (bottleneck) {
+        B.convs.push_back(conv(p + ".conv1", cin, width, 1, 1, 0, 0, false));
+        B.bns.push_back(bn(p + ".bn1", width));
+        B.convs.push_back(conv(p + ".conv2", width, width, 3, stride, 1, 0, false));
+        B.bns.push_back(bn(p + ".bn2", width));
+        B.convs.push_back(conv(p + ".conv3", width, cout, 1, 1, 0, 0, false));
+        B.bns.push_back(bn(p + ".bn3", cout));
+      } else {
+        B.convs.push_back(conv(p + ".conv1", cin, width, 3, stride, 1, 0, false));
+        B.bns.push_back(bn(p + ".bn1", width));
+        B.convs.push_back(conv(p + ".conv2", width, width, 3, 1, 1, 0, false));
+        B.bns.push_back(bn(p + ".bn2", width));
+      }
+      if (stride != 1 || cin != cout) {
+        B.down = true;
+        B.dconv = conv(p + ".down", cin, cout, 1, stride, 0, 0, false);
+        B.dbn = bn(p + ".down_bn", cout);
+      }
+      S.stages[si].push_back(B);
+      cin = cout;
+    }
+  }
+  const int enc18[5] = {64, 64, 128, 256, 512}, enc50[5] = {64, 256, 512, 1024, 2048};
+  for (int i = 0; i < 5; ++i) S.enc_ch[i] = bottleneck ? enc50[i] : enc18[i];
+  // DepthDecoder(; encoder_channels, scale_levels, embedding_levels=0) src/depth_decoder.jl:26-50
+  S.depth_begin = S.total;
+  const int dec[5] = {256, 128, 64, 32, 16};
+  int encr[5];
+  for (int i = 0; i < 5; ++i) encr[i] = S.enc_ch[4 - i];
+  const int in_ch[5] = {encr[0], dec[0], dec[1], dec[2], dec[3]};
+  const int skip[5] = {encr[1], encr[2], encr[3], encr[4], 0};
+  int bstart = 1;
+  for (int li = 0; li < a.nlevels; ++li) {
+    const int slevel = a.levels[li];
+    for (int bid = bstart; bid <= slevel; ++bid) {
+      const int b = bid - 1;
+      BranchSpec br;
+      br.bid = bid;
+      br.cin = in_ch[b];
+      br.cout = dec[b];
+      br.cskip = skip[b];
+      br.c1 = conv("depth.branch" + std::to_string(bid) + ".c1", in_ch[b], dec[b], 3, 1, 1, 1, true);
+      br.c2 = conv("depth.branch" + std::to_string(bid) + ".c2", dec[b] + skip[b], dec[b], 3, 1, 1, 1, true);
+      S.branches.push_back(br);
+    }
+    S.heads.push_back(conv("depth.head" + std::to_string(slevel), dec[slevel - 1], 1, 3, 1, 1, 1, true));
+    S.head_level.push_back(slevel);
+    S.branches.back().head = (int)S.heads.size() - 1;
+    bstart = slevel + 1;
+  }
+  // PoseDecoder(encoder_out_channels) src/pose_decoder.jl:13-21
+  S.squeezer = conv("pose.squeezer", S.enc_ch[4], 256, 1, 1, 0, 0, true);
+  S.p1 = conv("pose.conv1", 512, 256, 3, 1, 1, 0, true);
+  S.p2 = conv("pose.conv2", 256, 256, 3, 1, 1, 0, true);
+  S.p3 = conv("pose.conv3", 256, 6, 1, 1, 0, 0, true);
+  return S;
+}
+
+inline int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 1; }
+
+}  // namespace
+
+std::vector<ParamEntry> build_param_table(const ArchCfg& a) { return build_spec(a).table; }
+
+// ---------------------------------------------------------------------------------------------
+// runtime structures
+// ---------------------------------------------------------------------------------------------
+struct RConv {
+  PConv p;
+  ConvShape s{};          // N filled per call
+  float* wpf = nullptr;   // packed forward weights
+  float* wpd = nullptr;   // packed dgrad weights
+};
+struct RBN {
+  PBN p;
+  float *mean = nullptr, *invstd = nullptr, *rmean = nullptr, *rvar = nullptr;
+};
+struct EncStage {
+  RConv conv;
+  RBN bn;
+  float* y = nullptr;     // conv output
+  float* a = nullptr;     // post BN (+ReLU); block output for the last stage
+};
+struct EncBlock {
+  std::vector<EncStage> st;
+  bool down = false;
+  RConv dconv;
+  RBN dbn;
+  float* yd = nullptr;
+  float* in = nullptr;
+  float* d_in = nullptr;
+  float* d_out = nullptr;
+  int C = 0, H = 0, W = 0;      // output
+  int Cin = 0, Hin = 0, Win = 0;
+};
+struct DecBranch {
+  BranchSpec b;
+  RConv c1, c2;
+  int h = 0, w = 0;             // c1 resolution (input); output 2h x 2w
+  float *o1 = nullptr, *up = nullptr, *o2 = nullptr, *d_o2 = nullptr;
+  int head = -1;
+  RConv hc;
+  float* disp = nullptr;
+  float* d_head = nullptr;      // gradient w.r.t. the head pre-activation (from the loss tail)
+};
+
+class Model {
+ public:
+  ModelCfg cfg;
+  ArchSpec spec;
+  float* params = nullptr;
+  float* grads = nullptr;
+  std::vector<void*> allocs;
+  size_t bytes = 0;
+
+  int N = 0, B = 0;             // samples, encoder images (3N)
+  int H0 = 0, W0 = 0;           // stem output
+  int Hm = 0, Wm = 0;           // maxpool output
+  RConv stem;
+  RBN stem_bn;
+  float *y0 = nullptr, *f0 = nullptr, *mp = nullptr, *d_mp = nullptr, *d_f0 = nullptr;
+  unsigned char* mp_arg = nullptr;
+  std::vector<std::vector<EncBlock>> stages;
+  float* feat[5] = {};
+  int featC[5] = {}, featH[5] = {}, featW[5] = {};
+  std::vector<DecBranch> br;
+  float* d_skip[4] = {};
+  // pose
+  RConv sq, p1, p2, p3;
+  float *sqo = nullptr, *pc1 = nullptr, *pc2 = nullptr, *means = nullptr, *pose = nullptr;
+  float *d_pose = nullptr, *d_pc1 = nullptr, *d_pin = nullptr, *d_sq = nullptr;
+  // scratch
+  float *DA = nullptr, *DY = nullptr, *G = nullptr, *DYD = nullptr;
+  float *DPRE = nullptr, *DUP = nullptr, *DO1 = nullptr;
+  ConvWorkspace cws{};
+  BNStatsWs bnws{};
+  void* tail_ws = nullptr;
+  LossTailCfg tail{};
+  float* loss_buf = nullptr;
+  const float* eval_disp[MAX_SCALES] = {};
+
+  ~Model() {
+    for (void* p : allocs) (void)hipFree(p);
+  }
+
+  int alloc(float** p, size_t n) {
+    void* q = nullptr;
+    MD2_HIP(hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(float)));
+    allocs.push_back(q);
+    bytes += n * sizeof(float);
+    *p = (float*)q;
+    return MD2_OK;
+  }
+  float* P(long off) { return off >= 0 ? params + off : nullptr; }
+  float* Gd(long off) { return off >= 0 ? grads + off : nullptr; }
+
+  int make_conv(RConv& r, const PConv& p, int H, int W, bool dgrad, size_t& ws_need) {
+    r.p = p;
+    r.s.N = 0;
+    r.s.Cin = p.cin;
+    r.s.Cout = p.cout;
+    r.s.H = H;
+    r.s.W = W;
+    r.s.KH = r.s.KW = p.k;
+    r.s.stride = p.stride;
+    r.s.pad = p.pad;
+    r.s.reflect = p.reflect;
+    r.s.Ho = out_dim(H, p.k, p.stride, p.pad);
+    r.s.Wo = out_dim(W, p.k, p.stride, p.pad);
+    MD2_TRY(alloc(&r.wpf, conv_fwd_packed_elems(r.s)));
+    if (dgrad) MD2_TRY(alloc(&r.wpd, conv_dgrad_packed_elems(r.s)));
+    return MD2_OK;
+  }
+  void need_ws(const RConv& r, int nimg, size_t& ws_need, bool dgrad) {
+    ConvShape s = r.s;
+    s.N = nimg;
+    ws_need = std::max(ws_need, conv_fwd_workspace(s));
+    ws_need = std::max(ws_need, conv_wgrad_workspace(s));
+    if (dgrad) ws_need = std::max(ws_need, conv_dgrad_workspace(s));
+  }
+  int make_bn(RBN& r, const PBN& p) {
+    r.p = p;
+    MD2_TRY(alloc(&r.mean, p.c));
+    MD2_TRY(alloc(&r.invstd, p.c));
+    MD2_TRY(alloc(&r.rmean, p.c));
+    MD2_TRY(alloc(&r.rvar, p.c));
+    MD2_HIP(hipMemset(r.rmean, 0, p.c * sizeof(float)));
+    std::vector<float> ones(p.c, 1.f);
+    MD2_HIP(hipMemcpy(r.rvar, ones.data(), p.c * sizeof(float), hipMemcpyHostToDevice));
+    return MD2_OK;
+  }
+
+  int build() {
+    const ArchCfg& A = cfg.arch;
+    spec = build_spec(A);
+    N = cfg.N;
+    B = 3 * N;
+    const int C = A.in_ch;
+    size_t wsn = 0, scratch = 0;
+    long bnmax = 0;
+    auto track = [&](long n) { scratch = std::max(scratch, (size_t)n); };
+    auto bnws_need = [&](int Cc, long HW) {
+      bnmax = std::max(bnmax, (long)Cc * bn_parts(Cc, B, HW) * 2);
+    };
+    // ---- encoder
+    MD2_TRY(make_conv(stem, spec.stem, cfg.H, cfg.W, false, wsn));
+    need_ws(stem, B, wsn, false);
+    MD2_TRY(make_bn(stem_bn, spec.stem_bn));
+    H0 = stem.s.Ho;
+    W0 = stem.s.Wo;
+    Hm = out_dim(H0, 3, 2, 1);
+    Wm = out_dim(W0, 3, 2, 1);
+    const long n0 = (long)B * 64 * H0 * W0, nm = (long)B * 64 * Hm * Wm;
+    MD2_TRY(alloc(&y0, n0));
+    MD2_TRY(alloc(&f0, n0));
+    MD2_TRY(alloc(&d_f0, n0));
+    MD2_TRY(alloc(&mp, nm));
+    MD2_TRY(alloc(&d_mp, nm));
+    {
+      void* q;
+      MD2_HIP(hipMalloc(&q, nm));
+      allocs.push_back(q);
+      mp_arg = (unsigned char*)q;
+    }
+    track(n0);
+    bnws_need(64, (long)H0 * W0);
+    feat[0] = f0; featC[0] = 64; featH[0] = H0; featW[0] = W0;
+    float* cur = mp;
+    float* dcur = d_mp;
+    int cC = 64, cH = Hm, cW = Wm;
+    stages.resize(4);
+    for (int si = 0; si < 4; ++si) {
+      for (auto& bs : spec.stages[si]) {
+        EncBlock eb;
+        eb.in = cur;
+        eb.d_in = dcur;
+        eb.Cin = cC; eb.Hin = cH; eb.Win = cW;
+        int h = cH, w = cW;
+        for (size_t k = 0; k < bs.convs.size(); ++k) {
+          EncStage es;
+          MD2_TRY(make_conv(es.conv, bs.convs[k], h, w, true, wsn));
+          need_ws(es.conv, B, wsn, true);
+          MD2_TRY(make_bn(es.bn, bs.bns[k]));
+          h = es.conv.s.Ho;
+          w = es.conv.s.Wo;
+          const long n = (long)B * bs.convs[k].cout * h * w;
+          MD2_TRY(alloc(&es.y, n));
+          MD2_TRY(alloc(&es.a, n));
+          track(n);
+          bnws_need(bs.convs[k].cout, (long)h * w);
+          eb.st.push_back(es);
+        }
+        if (bs.down) {
+          eb.down = true;
+          MD2_TRY(make_conv(eb.dconv, bs.dconv, cH, cW, true, wsn));
+          need_ws(eb.dconv, B, wsn, true);
+          MD2_TRY(make_bn(eb.dbn, bs.dbn));
+          MD2_TRY(alloc(&eb.yd, (long)B * bs.cout * h * w));
+        }
+        eb.C = bs.cout; eb.H = h; eb.W = w;
+        MD2_TRY(alloc(&eb.d_out, (long)B * bs.cout * h * w));
+        cur = eb.st.back().a;
+        dcur = eb.d_out;
+        cC = bs.cout; cH = h; cW = w;
+        stages[si].push_back(eb);
+      }
+      feat[si + 1] = cur;
+      featC[si + 1] = cC; featH[si + 1] = cH; featW[si + 1] = cW;
+    }
+    // ---- depth decoder (N target images)
+    int h = featH[4], w = featW[4];
+    for (auto& bs : spec.branches) {
+      DecBranch d;
+      d.b = bs;
+      d.h = h;
+      d.w = w;
+      MD2_TRY(make_conv(d.c1, bs.c1, h, w, true, wsn));
+      need_ws(d.c1, N, wsn, true);
+      MD2_TRY(make_conv(d.c2, bs.c2, 2 * h, 2 * w, true, wsn));
+      need_ws(d.c2, N, wsn, true);
+      MD2_TRY(alloc(&d.o1, (long)N * bs.cout * h * w));
+      MD2_TRY(alloc(&d.up, (long)N * bs.cout * 4 * h * w));
+      MD2_TRY(alloc(&d.o2, (long)N * bs.cout * 4 * h * w));
+      MD2_TRY(alloc(&d.d_o2, (long)N * bs.cout * 4 * h * w));
+      track((long)N * (bs.cout + bs.cskip) * 4 * h * w);
+      if (bs.head >= 0) {
+        d.head = bs.head;
+        MD2_TRY(make_conv(d.hc, spec.heads[bs.head], 2 * h, 2 * w, true, wsn));
+        need_ws(d.hc, N, wsn, true);
+        MD2_TRY(alloc(&d.disp, (long)N * 4 * h * w));
+        MD2_TRY(alloc(&d.d_head, (long)N * 4 * h * w));
+      }
+      if (bs.bid <= 4) {
+        const int fi = 4 - bs.bid;
+        if (featH[fi] != 2 * h || featW[fi] != 2 * w) {
+          set_error("decoder/encoder resolution mismatch (image sides must be multiples of 32)");
+          return MD2_EINVAL;
+        }
+        MD2_TRY(alloc(&d_skip[fi], (long)N * featC[fi] * 4 * h * w));
+      }
+      h *= 2;
+      w *= 2;
+      br.push_back(d);
+    }
+    if (h != cfg.H || w != cfg.W) {
+      // the final branch must come back to full resolution for the loss (levels up to 5)
+    }
+    // ---- pose decoder (2N pairs)
+    const int h4 = featH[4], w4 = featW[4];
+    const long hw4 = (long)h4 * w4;
+    MD2_TRY(make_conv(sq, spec.squeezer, h4, w4, true, wsn));
+    need_ws(sq, B, wsn, true);
+    MD2_TRY(make_conv(p1, spec.p1, h4, w4, true, wsn));
+    need_ws(p1, 2 * N, wsn, true);
+    MD2_TRY(make_conv(p2, spec.p2, h4, w4, true, wsn));
+    need_ws(p2, 2 * N, wsn, true);
+    MD2_TRY(alloc(&sqo, (long)B * 256 * hw4));
+    MD2_TRY(alloc(&d_sq, (long)B * 256 * hw4));
+    MD2_TRY(alloc(&pc1, 2L * N * 256 * hw4));
+    MD2_TRY(alloc(&d_pc1, 2L * N * 256 * hw4));
+    MD2_TRY(alloc(&pc2, 2L * N * 256 * hw4));
+    MD2_TRY(alloc(&d_pin, 2L * N * 512 * hw4));
+    MD2_TRY(alloc(&means, 2L * N * 256));
+    MD2_TRY(alloc(&pose, 2L * N * 6));
+    MD2_TRY(alloc(&d_pose, 2L * N * 6));
+    track(2L * N * 512 * hw4);
+    // ---- scratch / workspaces
+    MD2_TRY(alloc(&DA, scratch));
+    MD2_TRY(alloc(&DY, scratch));
+    MD2_TRY(alloc(&G, scratch));
+    MD2_TRY(alloc(&DYD, scratch));
+    MD2_TRY(alloc(&DPRE, scratch));
+    MD2_TRY(alloc(&DUP, scratch));
+    MD2_TRY(alloc(&DO1, scratch));
+    {
+      float* q;
+      MD2_TRY(alloc(&q, wsn / sizeof(float) + 64));
+      cws.ptr = q;
+      cws.bytes = wsn + 256;
+    }
+    {
+      double* q;
+      void* v;
+      MD2_HIP(hipMalloc(&v, std::max<long>(bnmax, 2) * sizeof(double)));
+      allocs.push_back(v);
+      q = (double*)v;
+      bnws.partials = q;
+    }
+    // ---- loss tail (src/training.jl:21-78)
+    tail.N = N;
+    tail.C = C;
+    tail.W = cfg.W;
+    tail.H = cfg.H;
+    tail.nscales = A.nlevels;
+    int li = 0;
+    for (auto& d : br)
+      if (d.head >= 0) {
+        tail.dw[li] = 2 * d.w;
+        tail.dh[li] = 2 * d.h;
+        tail.smooth_w[li] = cfg.smoothness * cfg.scales[li];
+        ++li;
+      }
+    tail.divisor = (float)A.nlevels;
+    tail.smooth_normalize = 1;
+    std::memcpy(tail.K, cfg.K, sizeof(tail.K));
+    std::memcpy(tail.invK, cfg.invK, sizeof(tail.invK));
+    tail.min_depth = cfg.min_depth;
+    tail.max_depth = cfg.max_depth;
+    tail.x_frame_stride = (long)C * cfg.H * cfg.W;
+    tail.x_sample_stride = 3 * tail.x_frame_stride;
+    tail.target = cfg.target;
+    tail.src0 = cfg.src0;
+    tail.src1 = cfg.src1;
+    tail.invert_mask = (cfg.src0 < cfg.target ? 1 : 0) | (cfg.src1 < cfg.target ? 2 : 0);
+    tail.sigmoid_grad = 1;
+    {
+      float* q;
+      MD2_TRY(alloc(&q, loss_tail_workspace_bytes(tail) / sizeof(float) + 64));
+      tail_ws = q;
+    }
+    MD2_TRY(alloc(&loss_buf, 16));
+    return MD2_OK;
+  }
+
+  // -------------------------------------------------------------------------------------------
+  int conv_f(RConv& c, int nimg, const TensorIn& in, float* out, long out_bs, int act,
+             int accumulate, hipStream_t st) {
+    ConvShape s = c.s;
+    s.N = nimg;
+    TensorOut o;
+    o.p0 = out;
+    o.bs0 = out_bs;
+    o.bias = P(c.p.b);
+    o.act = act;
+    o.accumulate = accumulate;
+    return conv_fwd(s, in, c.wpf, o, cws, st);
+  }
+  static TensorIn tin(const float* p, int C, long HW) {
+    TensorIn t;
+    t.p0 = p;
+    t.c0 = C;
+    t.bs0 = (long)C * HW;
+    return t;
+  }
+
+  int repack(hipStream_t st) {
+    auto pk = [&](RConv& c) -> int {
+      MD2_TRY(conv_pack_fwd(c.s, params + c.p.w, c.wpf, st));
+      if (c.wpd) MD2_TRY(conv_pack_dgrad(c.s, params + c.p.w, c.wpd, st));
+      return MD2_OK;
+    };
+    MD2_TRY(pk(stem));
+    for (auto& sg : stages)
+      for (auto& b : sg) {
+        for (auto& e : b.st) MD2_TRY(pk(e.conv));
+        if (b.down) MD2_TRY(pk(b.dconv));
+      }
+    for (auto& d : br) {
+      MD2_TRY(pk(d.c1));
+      MD2_TRY(pk(d.c2));
+      if (d.head >= 0) MD2_TRY(pk(d.hc));
+    }
+    MD2_TRY(pk(sq));
+    MD2_TRY(pk(p1));
+    MD2_TRY(pk(p2));
+    return MD2_OK;
+  }
+
+  int bn_fwd(RBN& bn, const float* y, int nimg, long HW, hipStream_t st) {
+    BNStatsWs w = bnws;
+    w.parts = bn_parts(bn.p.c, nimg, HW);
+    return bn_stats(y, nimg, bn.p.c, HW, 1e-5f, 0.1f, bn.mean, bn.invstd, bn.rmean, bn.rvar, w, st);
+  }
+
+  // ---- encoder forward over nimg images (input already mapped by `in`)
+  int encoder_fwd(const TensorIn& in, int nimg, hipStream_t st) {
+    const long hw0 = (long)H0 * W0;
+    MD2_TRY(conv_f(stem, nimg, in, y0, 64 * hw0, ACT_NONE, 0, st));
+    MD2_TRY(bn_fwd(stem_bn, y0, nimg, hw0, st));
+    BNApply ap{};
+    ap.y = y0; ap.mean = stem_bn.mean; ap.invstd = stem_bn.invstd;
+    ap.gamma = P(stem_bn.p.g); ap.beta = P(stem_bn.p.b); ap.relu = 1;
+    MD2_TRY(bn_apply(ap, f0, nimg, 64, hw0, st));
+    MD2_TRY(maxpool_fwd(f0, nimg, 64, H0, W0, mp, mp_arg, Hm, Wm, st));
+    for (auto& sg : stages)
+      for (auto& b : sg) {
+        const float* x = b.in;
+        int C = b.Cin;
+        long HW = (long)b.Hin * b.Win;
+        for (size_t k = 0; k < b.st.size(); ++k) {
+          EncStage& e = b.st[k];
+          const long ohw = (long)e.conv.s.Ho * e.conv.s.Wo;
+          MD2_TRY(conv_f(e.conv, nimg, tin(x, C, HW), e.y, (long)e.conv.p.cout * ohw, ACT_NONE, 0, st));
+          MD2_TRY(bn_fwd(e.bn, e.y, nimg, ohw, st));
+          if (k + 1 < b.st.size()) {
+            BNApply a{};
+            a.y = e.y; a.mean = e.bn.mean; a.invstd = e.bn.invstd;
+            a.gamma = P(e.bn.p.g); a.beta = P(e.bn.p.b); a.relu = 1;
+            MD2_TRY(bn_apply(a, e.a, nimg, e.conv.p.cout, ohw, st));
+          }
+          x = e.a;
+          C = e.conv.p.cout;
+          HW = ohw;
+        }
+        EncStage& last = b.st.back();
+        const long ohw = (long)b.H * b.W;
+        BNApply a{};
+        a.y = last.y; a.mean = last.bn.mean; a.invstd = last.bn.invstd;
+        a.gamma = P(last.bn.p.g); a.beta = P(last.bn.p.b); a.relu = 1;
+        if (b.down) {
+          MD2_TRY(conv_f(b.dconv, nimg, tin(b.in, b.Cin, (long)b.Hin * b.Win), b.yd, (long)b.C * ohw, ACT_NONE, 0, st));
+          MD2_TRY(bn_fwd(b.dbn, b.yd, nimg, ohw, st));
+          a.y2 = b.yd; a.mean2 = b.dbn.mean; a.invstd2 = b.dbn.invstd;
+          a.gamma2 = P(b.dbn.p.g); a.beta2 = P(b.dbn.p.b);
+        } else {
+          a.res = b.in;
+        }
+        MD2_TRY(bn_apply(a, last.a, nimg, b.C, ohw, st));
+      }
+    return MD2_OK;
+  }
+
+  // ---- depth decoder over nimg images whose features start at image offset `img0`
+  int decoder_fwd(int nimg, int img0, hipStream_t st) {
+    const float* x = feat[4] + (long)img0 * featC[4] * featH[4] * featW[4];
+    int C = featC[4];
+    for (auto& d : br) {
+      const long hw = (long)d.h * d.w, hw2 = 4 * hw;
+      const int co = d.b.cout;
+      MD2_TRY(conv_f(d.c1, nimg, tin(x, C, hw), d.o1, co * hw, ACT_ELU, 0, st));
+      MD2_TRY(upsample2_fwd(d.o1, nimg, co, d.h, d.w, d.up, st));
+      TensorIn in = tin(d.up, co, hw2);
+      if (d.b.cskip > 0) {
+        const int fi = 4 - d.b.bid;
+        in.p1 = feat[fi] + (long)img0 * featC[fi] * hw2;
+        in.bs1 = (long)featC[fi] * hw2;
+      }
+      MD2_TRY(conv_f(d.c2, nimg, in, d.o2, co * hw2, ACT_ELU, 0, st));
+      if (d.head >= 0) MD2_TRY(conv_f(d.hc, nimg, tin(d.o2, co, hw2), d.disp, hw2, ACT_SIGMOID, 0, st));
+      x = d.o2;
+      C = co;
+    }
+    return MD2_OK;
+  }
+
+  int pose_fwd(hipStream_t st) {
+    const long hw4 = (long)featH[4] * featW[4];
+    MD2_TRY(conv_f(sq, B, tin(feat[4], featC[4], hw4), sqo, 256 * hw4, ACT_RELU, 0, st));
+    TensorIn in = tin(sqo, 256, hw4);
+    in.p1 = sqo + (long)N * 256 * hw4;   // pair (frame s, frame s+1) = images (q, q+N)
+    in.bs1 = 256 * hw4;
+    MD2_TRY(conv_f(p1, 2 * N, in, pc1, 256 * hw4, ACT_RELU, 0, st));
+    MD2_TRY(conv_f(p2, 2 * N, tin(pc1, 256, hw4), pc2, 256 * hw4, ACT_RELU, 0, st));
+    return pose_head_fwd(pc2, 2 * N, 256, hw4, P(spec.p3.w), P(spec.p3.b), means, pose, st);
+  }
+
+  int forward_loss(const float* x, const float* automask, float* loss, float* terms,
+                   hipStream_t st) {
+    const long fs = (long)cfg.arch.in_ch * cfg.H * cfg.W;
+    TensorIn in;
+    in.p0 = x;
+    in.c0 = cfg.arch.in_ch;
+    in.bdiv = N;          // image b = l*N + n  ->  x[n][l]
+    in.bs0 = 3 * fs;
+    in.bhi = fs;
+    MD2_TRY(encoder_fwd(in, B, st));
+    MD2_TRY(decoder_fwd(N, N, st));
+    MD2_TRY(pose_fwd(st));
+    const float* disps[MAX_SCALES] = {};
+    LossTailOut o{};
+    int li = 0;
+    for (auto& d : br)
+      if (d.head >= 0) {
+        disps[li] = d.disp;
+        o.d_disp[li] = d.d_head;
+        ++li;
+      }
+    o.loss = loss ? loss : loss_buf;
+    o.terms = terms;
+    o.d_pose = d_pose;
+    return loss_tail_run(tail, disps, pose, x, cfg.automask ? automask : nullptr, 1.f, o, tail_ws, st);
+  }
+
+  // -------------------------------------------------------------------------------------------
+  int conv_w(RConv& c, int nimg, const TensorIn& in, const float* dy, hipStream_t st) {
+    ConvShape s = c.s;
+    s.N = nimg;
+    return conv_wgrad(s, in, dy, grads + c.p.w, Gd(c.p.b), 0, cws, st);
+  }
+  int conv_d(RConv& c, int nimg, const float* dy, float* dx, long dx_bs, int acc, hipStream_t st,
+             float* dx1 = nullptr, long dx1_bs = 0, int c0 = 1 << 30) {
+    ConvShape s = c.s;
+    s.N = nimg;
+    TensorOut o;
+    o.p0 = dx;
+    o.bs0 = dx_bs;
+    o.p1 = dx1;
+    o.bs1 = dx1_bs;
+    o.c0 = c0;
+    o.accumulate = acc;
+    return conv_dgrad(s, dy, c.wpd, o, cws, st);
+  }
+  int bn_bwd(RBN& bn, const float* dout, const float* mask, const float* y, int nimg, long HW,
+             float* dy, float* dres, int dres_acc, hipStream_t st) {
+    BNStatsWs w = bnws;
+    w.parts = bn_parts(bn.p.c, nimg, HW);
+    MD2_TRY(bn_bwd_reduce(dout, mask, y, bn.mean, bn.invstd, nimg, bn.p.c, HW, Gd(bn.p.g),
+                          Gd(bn.p.b), w, st));
+    return bn_bwd_apply(dout, mask, y, bn.mean, bn.invstd, P(bn.p.g), Gd(bn.p.g), Gd(bn.p.b),
+                        nimg, bn.p.c, HW, dy, dres, dres_acc, st);
+  }
+
+  int block_bwd(EncBlock& b, hipStream_t st) {
+    const int nimg = B;
+    const long ohw = (long)b.H * b.W, ihw = (long)b.Hin * b.Win;
+    const int ns = (int)b.st.size();
+    EncStage& last = b.st.back();
+    // last BN (+ residual, ReLU): g = d_out * relu'(out)
+    MD2_TRY(bn_bwd(last.bn, b.d_out, last.a, last.y, nimg, ohw, DY, b.down ? G : b.d_in, 0, st));
+    if (b.down) {
+      MD2_TRY(bn_bwd(b.dbn, G, nullptr, b.yd, nimg, ohw, DYD, nullptr, 0, st));
+      MD2_TRY(conv_w(b.dconv, nimg, tin(b.in, b.Cin, ihw), DYD, st));
+      MD2_TRY(conv_d(b.dconv, nimg, DYD, b.d_in, (long)b.Cin * ihw, 0, st));
+    }
+    for (int k = ns - 1; k >= 0; --k) {
+      EncStage& e = b.st[k];
+      const float* xin = k == 0 ? b.in : b.st[k - 1].a;
+      const int cin = e.conv.p.cin;
+      const long hin = (long)e.conv.s.H * e.conv.s.W;
+      MD2_TRY(conv_w(e.conv, nimg, tin(xin, cin, hin), DY, st));
+      if (k > 0) {
+        MD2_TRY(conv_d(e.conv, nimg, DY, DA, (long)cin * hin, 0, st));
+        EncStage& pe = b.st[k - 1];
+        MD2_TRY(bn_bwd(pe.bn, DA, pe.a, pe.y, nimg, hin, DY, nullptr, 0, st));
+      } else {
+        MD2_TRY(conv_d(e.conv, nimg, DY, b.d_in, (long)cin * hin, 1, st));
+      }
+    }
+    return MD2_OK;
+  }
+
+  int seg_decoder(hipStream_t st) {
+    const long hw4 = (long)featH[4] * featW[4];
+    // ---- PoseDecoder backward
+    MD2_TRY(pose_head_bwd(d_pose, 2 * N, 256, hw4, P(spec.p3.w), means, DPRE, Gd(spec.p3.w),
+                          Gd(spec.p3.b), st));
+    MD2_TRY(act_backward(pc2, DPRE, DPRE, 2L * N * 256 * hw4, ACT_RELU, st));
+    MD2_TRY(conv_w(p2, 2 * N, tin(pc1, 256, hw4), DPRE, st));
+    MD2_TRY(conv_d(p2, 2 * N, DPRE, d_pc1, 256 * hw4, 0, st));
+    MD2_TRY(act_backward(pc1, d_pc1, d_pc1, 2L * N * 256 * hw4, ACT_RELU, st));
+    TensorIn pin = tin(sqo, 256, hw4);
+    pin.p1 = sqo + (long)N * 256 * hw4;
+    pin.bs1 = 256 * hw4;
+    MD2_TRY(conv_w(p1, 2 * N, pin, d_pc1, st));
+    MD2_TRY(conv_d(p1, 2 * N, d_pc1, d_pin, 512 * hw4, 0, st));
+    MD2_TRY(pair_grad_gather(d_pin, N, 256, hw4, d_sq, st));
+    MD2_TRY(act_backward(sqo, d_sq, d_sq, (long)B * 256 * hw4, ACT_RELU, st));
+    MD2_TRY(conv_w(sq, B, tin(feat[4], featC[4], hw4), d_sq, st));
+    float* d_f4 = stages[3].back().d_out;
+    MD2_TRY(conv_d(sq, B, d_sq, d_f4, (long)featC[4] * hw4, 0, st));
+    // ---- DepthDecoder backward (reverse branch order)
+    const int nb = (int)br.size();
+    for (int i = nb - 1; i >= 0; --i) {
+      DecBranch& d = br[i];
+      const long hw = (long)d.h * d.w, hw2 = 4 * hw;
+      const int co = d.b.cout;
+      if (d.head >= 0) {
+        MD2_TRY(conv_w(d.hc, N, tin(d.o2, co, hw2), d.d_head, st));
+        MD2_TRY(conv_d(d.hc, N, d.d_head, d.d_o2, co * hw2, i < nb - 1 ? 1 : 0, st));
+      }
+      MD2_TRY(act_backward(d.o2, d.d_o2, DPRE, (long)N * co * hw2, ACT_ELU, st));
+      TensorIn in = tin(d.up, co, hw2);
+      float* dskip = nullptr;
+      long skip_bs = 0;
+      if (d.b.cskip > 0) {
+        const int fi = 4 - d.b.bid;
+        in.p1 = feat[fi] + (long)N * featC[fi] * hw2;
+        in.bs1 = (long)featC[fi] * hw2;
+        dskip = d_skip[fi];
+        skip_bs = (long)featC[fi] * hw2;
+      }
+      MD2_TRY(conv_w(d.c2, N, in, DPRE, st));
+      MD2_TRY(conv_d(d.c2, N, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
+      MD2_TRY(upsample2_bwd(DUP, N, co, d.h, d.w, DO1, st));
+      MD2_TRY(act_backward(d.o1, DO1, DO1, (long)N * co * hw, ACT_ELU, st));
+      const float* xin;
+      int cin;
+      float* dx;
+      int acc;
+      if (i == 0) {
+        cin = featC[4];
+        xin = feat[4] + (long)N * cin * hw;
+        dx = d_f4 + (long)N * cin * hw;
+        acc = 1;
+      } else {
+        cin = br[i - 1].b.cout;
+        xin = br[i - 1].o2;
+        dx = br[i - 1].d_o2;
+        acc = 0;
+      }
+      MD2_TRY(conv_w(d.c1, N, tin(xin, cin, hw), DO1, st));
+      MD2_TRY(conv_d(d.c1, N, DO1, dx, (long)cin * hw, acc, st));
+    }
+    return MD2_OK;
+  }
+
+  int seg_stage(int si, hipStream_t st) {
+    auto& sg = stages[si];
+    for (int k = (int)sg.size() - 1; k >= 0; --k) MD2_TRY(block_bwd(sg[k], st));
+    if (si >= 1) {
+      // d f_si (= block 0's d_in) += decoder skip gradient on the target slice
+      const long n = (long)N * featC[si] * featH[si] * featW[si];
+      MD2_TRY(axpy(sg[0].d_in + n, d_skip[si], n, st));
+    }
+    return MD2_OK;
+  }
+
+  int seg_stem(hipStream_t st) {
+    const long hw0 = (long)H0 * W0;
+    MD2_TRY(maxpool_bwd(d_mp, mp_arg, B, 64, H0, W0, Hm, Wm, d_f0, st));
+    const long n = (long)N * 64 * hw0;
+    MD2_TRY(axpy(d_f0 + n, d_skip[0], n, st));
+    MD2_TRY(bn_bwd(stem_bn, d_f0, f0, y0, B, hw0, DY, nullptr, 0, st));
+    const long fs = (long)cfg.arch.in_ch * cfg.H * cfg.W;
+    TensorIn in;
+    in.p0 = cur_x;
+    in.c0 = cfg.arch.in_ch;
+    in.bdiv = N;
+    in.bs0 = 3 * fs;
+    in.bhi = fs;
+    return conv_w(stem, B, in, DY, st);
+  }
+
+  const float* cur_x = nullptr;
+};
+
+// ---------------------------------------------------------------------------------------------
+int model_create(const ModelCfg& cfg, float* params, float* grads, Model** out) {
+  MD2_CHECK_ARG(out != nullptr && params != nullptr && grads != nullptr, "model_create args");
+  MD2_CHECK_ARG(cfg.arch.arch == 18 || cfg.arch.arch == 34 || cfg.arch.arch == 50, "arch 18/34/50");
+  MD2_CHECK_ARG(cfg.arch.in_ch == 1 || cfg.arch.in_ch == 3, "in_channels 1 or 3");
+  MD2_CHECK_ARG(cfg.N >= 1 && cfg.W % 32 == 0 && cfg.H % 32 == 0 && cfg.W >= 64 && cfg.H >= 64,
+                "width/height must be multiples of 32 (>= 64)");
+  MD2_CHECK_ARG(cfg.target == 1 && cfg.src0 == 0 && cfg.src1 == 2,
+                "the HIP model supports target_id=2, source_ids=[1,3] (Depth10k/KITTI triplets)");
+  MD2_CHECK_ARG(cfg.arch.nlevels >= 1 && cfg.arch.nlevels <= 4, "scale levels");
+  for (int i = 0; i < cfg.arch.nlevels; ++i)
+    MD2_CHECK_ARG(cfg.arch.levels[i] >= 2 && cfg.arch.levels[i] <= 5 &&
+                      (i == 0 || cfg.arch.levels[i] > cfg.arch.levels[i - 1]),
+                  "scale_levels must be increasing in 2:5");
+  MD2_CHECK_ARG(cfg.arch.levels[cfg.arch.nlevels - 1] == 5, "the last scale level must be 5 (full res)");
+  Model* m = new Model();
+  m->cfg = cfg;
+  m->params = params;
+  m->grads = grads;
+  int rc = m->build();
+  if (rc) {
+    delete m;
+    return rc;
+  }
+  *out = m;
+  return MD2_OK;
+}
+
+void model_destroy(Model* m) { delete m; }
+
+int model_forward_loss(Model* m, const float* x, const float* automask, float* loss, float* terms,
+                       hipStream_t st) {
+  MD2_CHECK_ARG(m && x, "model/x");
+  MD2_CHECK_ARG(!m->cfg.automask || automask, "automasking needs auto_loss");
+  m->cur_x = x;
+  return m->forward_loss(x, automask, loss, terms, st);
+}
+
+int model_num_segments(Model* m) { return m ? 6 : 0; }
+
+int model_backward_segment(Model* m, int k, long* off, long* len, hipStream_t st) {
+  MD2_CHECK_ARG(m && m->cur_x, "backward before forward");
+  MD2_CHECK_ARG(k >= 0 && k < 6, "segment index");
+  long b = 0, e = 0;
+  const ArchSpec& S = m->spec;
+  switch (k) {
+    case 0: MD2_TRY(m->seg_decoder(st)); b = S.depth_begin; e = S.total; break;
+    case 1: MD2_TRY(m->seg_stage(3, st)); b = S.stage_begin[4]; e = S.depth_begin; break;
+    case 2: MD2_TRY(m->seg_stage(2, st)); b = S.stage_begin[3]; e = S.stage_begin[4]; break;
+    case 3: MD2_TRY(m->seg_stage(1, st)); b = S.stage_begin[2]; e = S.stage_begin[3]; break;
+    case 4: MD2_TRY(m->seg_stage(0, st)); b = S.stage_begin[1]; e = S.stage_begin[2]; break;
+    default: MD2_TRY(m->seg_stem(st)); b = 0; e = S.stage_begin[1]; break;
+  }
+  if (off) *off = b;
+  if (len) *len = e - b;
+  return MD2_OK;
+}
+
+int model_adam(Model* m, float* adam_m, float* adam_v, float lr, float b1, float b2, float eps,
+               int step, float grad_scale, hipStream_t st) {
+  MD2_CHECK_ARG(m && adam_m && adam_v && step >= 1, "adam args");
+  const double bc1 = 1.0 - std::pow((double)b1, step), bc2 = 1.0 - std::pow((double)b2, step);
+  MD2_TRY(adam_step(m->params, m->grads, adam_m, adam_v, m->spec.total, lr, b1, b2, eps, (float)bc1,
+                    (float)bc2, grad_scale, st));
+  return m->repack(st);
+}
+
+int model_repack(Model* m, hipStream_t st) {
+  MD2_CHECK_ARG(m, "model");
+  return m->repack(st);
+}
+
+int model_outputs(Model* m, const float** disp, int* dw, int* dh, const float** pose) {
+  MD2_CHECK_ARG(m, "model");
+  int li = 0;
+  for (auto& d : m->br)
+    if (d.head >= 0) {
+      if (disp) disp[li] = d.disp;
+      if (dw) dw[li] = 2 * d.w;
+      if (dh) dh[li] = 2 * d.h;
+      ++li;
+    }
+  if (pose) *pose = m->pose;
+  return MD2_OK;
+}
+
+int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipStream_t st) {
+  MD2_CHECK_ARG(m && x && n >= 1 && n <= m->N, "eval_disparity: 1 <= n <= batch");
+  TensorIn in = Model::tin(x, m->cfg.arch.in_ch, (long)m->cfg.H * m->cfg.W);
+  MD2_TRY(m->encoder_fwd(in, n, st));
+  MD2_TRY(m->decoder_fwd(n, 0, st));
+  if (disp_out) {
+    int li = 0;
+    for (auto& d : m->br)
+      if (d.head >= 0) disp_out[li++] = d.disp;
+  }
+  return MD2_OK;
+}
+
+long model_param_count(Model* m) { return m ? m->spec.total : 0; }
+size_t model_device_bytes(Model* m) { return m ? m->bytes : 0; }
+
+}  // namespace md2

@@ -1,0 +1,63 @@
+// Model executor: Model(encoder, DepthDecoder, PoseDecoder) forward + train_loss + backward +
+// ADAM on the HIP kernels (src/model.jl, src/depth_decoder.jl, src/pose_decoder.jl,
+// src/training.jl; encoder = ResNet.jl ResidualNetwork with torchvision topology).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "conv.h"
+#include "loss_tail.h"
+#include "nn.h"
+
+namespace md2 {
+
+struct ArchCfg {
+  int arch = 18;           // 18 / 34 / 50
+  int in_ch = 3;
+  int nlevels = 4;
+  int levels[MAX_SCALES] = {2, 3, 4, 5};
+};
+
+struct ParamEntry {
+  std::string name;
+  int ndim;
+  int shape[4];
+  long offset;
+  long numel;
+};
+
+// flat parameter table in the order of oracle/md2_oracle.py param_spec
+std::vector<ParamEntry> build_param_table(const ArchCfg& a);
+
+struct ModelCfg {
+  ArchCfg arch;
+  int N, W, H;             // samples per step, target size
+  float K[9], invK[9];
+  float min_depth = 0.1f, max_depth = 100.f, smoothness = 1e-3f;
+  float scales[MAX_SCALES] = {0.125f, 0.25f, 0.5f, 1.f};
+  int automask = 0;
+  int target = 1, src0 = 0, src1 = 2;   // 0-based frame ids, L = 3
+};
+
+class Model;
+int model_create(const ModelCfg& cfg, float* params, float* grads, Model** out);
+void model_destroy(Model* m);
+
+// train path
+int model_forward_loss(Model* m, const float* x, const float* automask, float* loss, float* terms,
+                       hipStream_t st);
+int model_num_segments(Model* m);
+// runs backward segment k (0 = pose+decoder ... last = stem); [off, off+len) of the flat gradient
+// is final afterwards
+int model_backward_segment(Model* m, int k, long* off, long* len, hipStream_t st);
+int model_adam(Model* m, float* adam_m, float* adam_v, float lr, float b1, float b2, float eps,
+               int step, float grad_scale, hipStream_t st);
+int model_repack(Model* m, hipStream_t st);   // after the parameters changed
+// outputs of the last forward
+int model_outputs(Model* m, const float** disp, int* dw, int* dh, const float** pose);
+// inference: eval_disparity (src/model.jl:63) on x [n][C][H][W], n <= N*3
+int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipStream_t st);
+long model_param_count(Model* m);
+size_t model_device_bytes(Model* m);
+
+}  // namespace md2

@@ -1,0 +1,60 @@
+// Non-GEMM layers of the train step: BatchNorm (train mode), max-pool, x2 bilinear upsample,
+// the pose head (1x1 conv + spatial mean), Adam, small elementwise helpers.
+#pragma once
+#include "common.h"
+
+namespace md2 {
+
+// ---- BatchNorm, Flux train mode (batch mean / biased var, eps), per channel over N*HW ----
+struct BNStatsWs {
+  double* partials;   // [C][parts][2]
+  int parts;
+};
+int bn_parts(int C, long N, long HW);
+// mean/invstd [C]; running stats updated when run_mean != nullptr (momentum, unbiased var)
+int bn_stats(const float* y, int N, int C, long HW, float eps, float momentum, float* mean,
+             float* invstd, float* run_mean, float* run_var, BNStatsWs ws, hipStream_t st);
+// out = act(gamma*(y-mean)*invstd + beta [+ gamma2*(y2-mean2)*invstd2 + beta2] [+ res])
+struct BNApply {
+  const float* y; const float* mean; const float* invstd; const float* gamma; const float* beta;
+  const float* y2 = nullptr; const float* mean2 = nullptr; const float* invstd2 = nullptr;
+  const float* gamma2 = nullptr; const float* beta2 = nullptr;
+  const float* res = nullptr;
+  int relu = 0;
+};
+int bn_apply(const BNApply& p, float* out, int N, int C, long HW, hipStream_t st);
+// backward reduce: g = dout * (mask_out > 0 if mask_out) ; dgamma = sum g*xhat, dbeta = sum g
+int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, const float* mean,
+                  const float* invstd, int N, int C, long HW, float* dgamma, float* dbeta,
+                  BNStatsWs ws, hipStream_t st);
+// dy = gamma*invstd*(g - dbeta/L - xhat*dgamma/L); optional dres (=g) store/accumulate
+int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const float* mean,
+                 const float* invstd, const float* gamma, const float* dgamma,
+                 const float* dbeta, int N, int C, long HW, float* dy, float* dres,
+                 int dres_accumulate, hipStream_t st);
+
+// ---- MaxPool((3,3); stride 2, pad 1) ----
+int maxpool_fwd(const float* x, int N, int C, int H, int W, float* y, unsigned char* arg,
+                int Ho, int Wo, hipStream_t st);
+int maxpool_bwd(const float* dy, const unsigned char* arg, int N, int C, int H, int W, int Ho,
+                int Wo, float* dx, hipStream_t st);
+
+// ---- upsample_bilinear(x, (2,2)), align_corners = true ----
+int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStream_t st);
+int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStream_t st);
+
+// ---- pose head: pose[q][k] = 0.01 * (b[k] + sum_c W[k][c] * mean_hw(x[q][c])) ----
+int pose_head_fwd(const float* x, int Q, int C, long HW, const float* w, const float* b,
+                  float* means, float* pose, hipStream_t st);
+int pose_head_bwd(const float* dpose, int Q, int C, long HW, const float* w, const float* means,
+                  float* dx, float* dw, float* db, hipStream_t st);
+
+// ---- misc elementwise ----
+int axpy(float* y, const float* x, long n, hipStream_t st);               // y += x
+int pair_grad_gather(const float* dpin, int N, int C, long HW, float* dsq, hipStream_t st);
+
+// ---- Flux ADAM over the flat parameter vector ----
+int adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
+              float eps, float bc1, float bc2, float gscale, hipStream_t st);
+
+}  // namespace md2

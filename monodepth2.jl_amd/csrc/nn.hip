@@ -1,0 +1,510 @@
+// Non-GEMM layers of the train step (see nn.h).  All are HBM-bound streaming kernels; channel
+// reductions are deterministic two-stage (per-block fp64 partials, then a per-channel finalise).
+#include "nn.h"
+
+namespace md2 {
+
+// ---------------------------------------------------------------------------------------------
+// BatchNorm (Flux BatchNorm in trainmode!: batch statistics, biased variance, eps = 1e-5)
+// ---------------------------------------------------------------------------------------------
+int bn_parts(int C, long N, long HW) {
+  long total = N * HW;
+  int parts = (int)std::max(1L, std::min(1024L / std::max(1, C) + 1, total / 2048 + 1));
+  return std::min(parts, 256);
+}
+
+// one block per (channel, part); sums over a contiguous slice of the N*HW elements
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ y, int C,
+                                                               long HW, long total, int parts,
+                                                               double* __restrict__ part) {
+  __shared__ double red[8];
+  const int c = blockIdx.x, p = blockIdx.y;
+  const long beg = total * p / parts, end = total * (p + 1) / parts;
+  double s = 0.0, ss = 0.0;
+  for (long e = beg + threadIdx.x; e < end; e += 256) {
+    const long img = e / HW, pix = e - img * HW;
+    const double v = y[(img * C + c) * HW + pix];
+    s += v;
+    ss += v * v;
+  }
+  s = wave_sum_d(s);
+  ss = wave_sum_d(ss);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[wid] = s;
+    red[4 + wid] = ss;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[((long)c * parts + p) * 2 + 0] = red[0] + red[1] + red[2] + red[3];
+    part[((long)c * parts + p) * 2 + 1] = red[4] + red[5] + red[6] + red[7];
+  }
+}
+
+__global__ void bn_stats_final_kernel(const double* __restrict__ part, int C, int parts,
+                                      long total, float eps, float momentum, float* mean,
+                                      float* invstd, float* run_mean, float* run_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, ss = 0.0;
+  for (int p = 0; p < parts; ++p) {
+    s += part[((long)c * parts + p) * 2];
+    ss += part[((long)c * parts + p) * 2 + 1];
+  }
+  const double mu = s / (double)total;
+  const double var = fmax(ss / (double)total - mu * mu, 0.0);
+  mean[c] = (float)mu;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean) {
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mu;
+    run_var[c] = (1.f - momentum) * run_var[c] +
+                 momentum * (float)(var * (double)total / (double)std::max(total - 1, 1L));
+  }
+}
+
+int bn_stats(const float* y, int N, int C, long HW, float eps, float momentum, float* mean,
+             float* invstd, float* run_mean, float* run_var, BNStatsWs ws, hipStream_t st) {
+  const long total = (long)N * HW;
+  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(C, ws.parts), dim3(256), 0, st, y, C, HW, total,
+                     ws.parts, ws.partials);
+  MD2_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(cdiv(C, 64)), dim3(64), 0, st, ws.partials, C,
+                     ws.parts, total, eps, momentum, mean, invstd, run_mean, run_var);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// float4 over [N][C][HW] with HW % 4 == 0 (all encoder maps) or scalar fallback
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_apply_kernel(BNApply p, float* __restrict__ out, int C,
+                                                       long HW, long n) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * (VEC ? 4 : 1);
+  if (i >= n) return;
+  const int c = (int)((i / HW) % C);
+  const float sc = p.gamma[c] * p.invstd[c], sh = p.beta[c] - p.mean[c] * sc;
+  float sc2 = 0.f, sh2 = 0.f;
+  if (p.y2) {
+    sc2 = p.gamma2[c] * p.invstd2[c];
+    sh2 = p.beta2[c] - p.mean2[c] * sc2;
+  }
+  if (VEC) {
+    float4 v = *reinterpret_cast<const float4*>(p.y + i);
+    float r[4] = {v.x * sc + sh, v.y * sc + sh, v.z * sc + sh, v.w * sc + sh};
+    if (p.y2) {
+      const float4 u = *reinterpret_cast<const float4*>(p.y2 + i);
+      r[0] += u.x * sc2 + sh2; r[1] += u.y * sc2 + sh2; r[2] += u.z * sc2 + sh2; r[3] += u.w * sc2 + sh2;
+    }
+    if (p.res) {
+      const float4 u = *reinterpret_cast<const float4*>(p.res + i);
+      r[0] += u.x; r[1] += u.y; r[2] += u.z; r[3] += u.w;
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = fmaxf(r[k], 0.f);
+    }
+    *reinterpret_cast<float4*>(out + i) = make_float4(r[0], r[1], r[2], r[3]);
+  } else {
+    float r = p.y[i] * sc + sh;
+    if (p.y2) r += p.y2[i] * sc2 + sh2;
+    if (p.res) r += p.res[i];
+    if (p.relu) r = fmaxf(r, 0.f);
+    out[i] = r;
+  }
+}
+
+int bn_apply(const BNApply& p, float* out, int N, int C, long HW, hipStream_t st) {
+  const long n = (long)N * C * HW;
+  if (HW % 4 == 0) {
+    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st, p, out, C, HW, n);
+  } else {
+    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st, p, out, C, HW, n);
+  }
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
+    const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int C, long HW, long total,
+    int parts, double* __restrict__ part) {
+  __shared__ double red[8];
+  const int c = blockIdx.x, p = blockIdx.y;
+  const long beg = total * p / parts, end = total * (p + 1) / parts;
+  const float mu = mean[c], is = invstd[c];
+  double sg = 0.0, sgx = 0.0;
+  for (long e = beg + threadIdx.x; e < end; e += 256) {
+    const long img = e / HW, pix = e - img * HW;
+    const long idx = (img * C + c) * HW + pix;
+    float g = dout[idx];
+    if (mask && !(mask[idx] > 0.f)) g = 0.f;
+    sg += g;
+    sgx += (double)g * (double)((y[idx] - mu) * is);
+  }
+  sg = wave_sum_d(sg);
+  sgx = wave_sum_d(sgx);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[wid] = sg;
+    red[4 + wid] = sgx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[((long)c * parts + p) * 2 + 0] = red[0] + red[1] + red[2] + red[3];
+    part[((long)c * parts + p) * 2 + 1] = red[4] + red[5] + red[6] + red[7];
+  }
+}
+
+__global__ void bn_bwd_final_kernel(const double* __restrict__ part, int C, int parts,
+                                    float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int p = 0; p < parts; ++p) {
+    sg += part[((long)c * parts + p) * 2];
+    sgx += part[((long)c * parts + p) * 2 + 1];
+  }
+  dbeta[c] = (float)sg;
+  dgamma[c] = (float)sgx;
+}
+
+int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, const float* mean,
+                  const float* invstd, int N, int C, long HW, float* dgamma, float* dbeta,
+                  BNStatsWs ws, hipStream_t st) {
+  const long total = (long)N * HW;
+  hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(C, ws.parts), dim3(256), 0, st, dout, mask_out, y,
+                     mean, invstd, C, HW, total, ws.parts, ws.partials);
+  MD2_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 64)), dim3(64), 0, st, ws.partials, C,
+                     ws.parts, dgamma, dbeta);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ dgamma,
+    const float* __restrict__ dbeta, int C, long HW, long n, float invL, float* __restrict__ dy,
+    float* __restrict__ dres, int dres_acc) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)((i / HW) % C);
+  float g = dout[i];
+  if (mask && !(mask[i] > 0.f)) g = 0.f;
+  const float is = invstd[c];
+  const float xh = (y[i] - mean[c]) * is;
+  dy[i] = gamma[c] * is * (g - dbeta[c] * invL - xh * dgamma[c] * invL);
+  if (dres) {
+    if (dres_acc)
+      dres[i] += g;
+    else
+      dres[i] = g;
+  }
+}
+
+int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const float* mean,
+                 const float* invstd, const float* gamma, const float* dgamma,
+                 const float* dbeta, int N, int C, long HW, float* dy, float* dres,
+                 int dres_accumulate, hipStream_t st) {
+  const long n = (long)N * C * HW;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dout, mask_out, y,
+                     mean, invstd, gamma, dgamma, dbeta, C, HW, n, 1.f / (float)((long)N * HW), dy,
+                     dres, dres_accumulate);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// MaxPool 3x3 / stride 2 / pad 1 (ResNet stem); argmax kept as the window index 0..8
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restrict__ x, int H, int W,
+                                                          float* __restrict__ y,
+                                                          unsigned char* __restrict__ arg, int Ho,
+                                                          int Wo, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int ow = (int)(i % Wo), oh = (int)((i / Wo) % Ho);
+  const long plane = i / ((long)Ho * Wo);
+  const float* p = x + plane * H * W;
+  float best = -INFINITY;
+  int bi = 0;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int ih = oh * 2 - 1 + kh;
+    if (ih < 0 || ih >= H) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int iw = ow * 2 - 1 + kw;
+      if (iw < 0 || iw >= W) continue;
+      const float v = p[ih * W + iw];
+      if (v > best) {
+        best = v;
+        bi = kh * 3 + kw;
+      }
+    }
+  }
+  y[i] = best;
+  arg[i] = (unsigned char)bi;
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ dy,
+                                                          const unsigned char* __restrict__ arg,
+                                                          int H, int W, int Ho, int Wo,
+                                                          float* __restrict__ dx, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int iw = (int)(i % W), ih = (int)((i / W) % H);
+  const long plane = i / ((long)H * W);
+  const float* g = dy + plane * Ho * Wo;
+  const unsigned char* a = arg + plane * Ho * Wo;
+  float s = 0.f;
+  const int oh_lo = max(0, (ih - 1 + 1) / 2), oh_hi = min(Ho - 1, (ih + 1) / 2);
+  const int ow_lo = max(0, (iw - 1 + 1) / 2), ow_hi = min(Wo - 1, (iw + 1) / 2);
+  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+    const int kh = ih - (oh * 2 - 1);
+    if (kh < 0 || kh > 2) continue;
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      const int kw = iw - (ow * 2 - 1);
+      if (kw < 0 || kw > 2) continue;
+      if (a[oh * Wo + ow] == kh * 3 + kw) s += g[oh * Wo + ow];
+    }
+  }
+  dx[i] = s;
+}
+
+int maxpool_fwd(const float* x, int N, int C, int H, int W, float* y, unsigned char* arg, int Ho,
+                int Wo, hipStream_t st) {
+  const long n = (long)N * C * Ho * Wo;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, x, H, W, y, arg, Ho, Wo, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int maxpool_bwd(const float* dy, const unsigned char* arg, int N, int C, int H, int W, int Ho,
+                int Wo, float* dx, hipStream_t st) {
+  const long n = (long)N * C * H * W;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, arg, H, W, Ho, Wo, dx, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// upsample_bilinear(x, (2,2)) with align_corners = true (src/depth_decoder.jl:18-19)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void src_idx(int o, float r, int in, int& i0, int& i1, float& f) {
+  const float s = r * (float)o;
+  i0 = min((int)s, in - 1);
+  i1 = min(i0 + 1, in - 1);
+  f = s - (float)i0;
+}
+
+__global__ __launch_bounds__(256) void upsample2_fwd_kernel(const float* __restrict__ x, int h,
+                                                            int w, float ry, float rx,
+                                                            float* __restrict__ y, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int W2 = 2 * w, H2 = 2 * h;
+  const int ox = (int)(i % W2), oy = (int)((i / W2) % H2);
+  const long plane = i / ((long)H2 * W2);
+  const float* p = x + plane * h * w;
+  int y0, y1, x0, x1;
+  float fy, fx;
+  src_idx(oy, ry, h, y0, y1, fy);
+  src_idx(ox, rx, w, x0, x1, fx);
+  y[i] = (1.f - fy) * ((1.f - fx) * p[y0 * w + x0] + fx * p[y0 * w + x1]) +
+         fy * ((1.f - fx) * p[y1 * w + x0] + fx * p[y1 * w + x1]);
+}
+
+__device__ __forceinline__ float up_w(int o, int j, float r, int in) {
+  int i0, i1;
+  float f;
+  src_idx(o, r, in, i0, i1, f);
+  return (i0 == j ? 1.f - f : 0.f) + (i1 == j ? f : 0.f);
+}
+
+// gather adjoint: input pixel (iy, ix) collects the output pixels whose 2x2 stencil touches it
+__global__ __launch_bounds__(256) void upsample2_bwd_kernel(const float* __restrict__ dy, int h,
+                                                            int w, float ry, float rx,
+                                                            float* __restrict__ dx, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int W2 = 2 * w, H2 = 2 * h;
+  const int ix = (int)(i % w), iy = (int)((i / w) % h);
+  const long plane = i / ((long)h * w);
+  const float* g = dy + plane * H2 * W2;
+  // outputs o with floor(o*r) in {i-1, i}:  o in [(i-1)/r, (i+1)/r]
+  const int ylo = (h == 1) ? 0 : max(0, (int)floorf((float)(iy - 1) / ry) - 1);
+  const int yhi = (h == 1) ? H2 - 1 : min(H2 - 1, (int)ceilf((float)(iy + 1) / ry) + 1);
+  const int xlo = (w == 1) ? 0 : max(0, (int)floorf((float)(ix - 1) / rx) - 1);
+  const int xhi = (w == 1) ? W2 - 1 : min(W2 - 1, (int)ceilf((float)(ix + 1) / rx) + 1);
+  float s = 0.f;
+  for (int oy = ylo; oy <= yhi; ++oy) {
+    const float wy = up_w(oy, iy, ry, h);
+    if (wy == 0.f) continue;
+    float row = 0.f;
+    for (int ox = xlo; ox <= xhi; ++ox) {
+      const float wx = up_w(ox, ix, rx, w);
+      if (wx != 0.f) row += wx * g[oy * W2 + ox];
+    }
+    s += wy * row;
+  }
+  dx[i] = s;
+}
+
+static inline float up_ratio(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
+
+int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStream_t st) {
+  const long n = (long)N * C * 4 * h * w;
+  hipLaunchKernelGGL(upsample2_fwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, x, h, w,
+                     up_ratio(h, 2 * h), up_ratio(w, 2 * w), y, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStream_t st) {
+  const long n = (long)N * C * h * w;
+  hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, h, w,
+                     up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pose head: Conv((1,1), 256=>6) + mean over (w,h) + 1e-2 scale (src/pose_decoder.jl:19,29-30).
+// mean(W x + b) = W mean(x) + b, so the 1x1 conv runs on the spatial means.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pose_means_kernel(const float* __restrict__ x, int C, long HW,
+                                                         float* __restrict__ means) {
+  const int q = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float* p = x + ((long)q * C + c) * HW;
+    float s = 0.f;
+    for (long i = 0; i < HW; ++i) s += p[i];
+    means[(long)q * C + c] = s / (float)HW;
+  }
+}
+
+__global__ __launch_bounds__(64) void pose_fc_kernel(const float* __restrict__ means, int C,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ b,
+                                                     float* __restrict__ pose) {
+  const int q = blockIdx.x, k = blockIdx.y;
+  float s = 0.f;
+  for (int c = threadIdx.x; c < C; c += 64) s += w[(long)k * C + c] * means[(long)q * C + c];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) pose[q * 6 + k] = 1e-2f * (s + b[k]);
+}
+
+int pose_head_fwd(const float* x, int Q, int C, long HW, const float* w, const float* b,
+                  float* means, float* pose, hipStream_t st) {
+  hipLaunchKernelGGL(pose_means_kernel, dim3(Q), dim3(256), 0, st, x, C, HW, means);
+  MD2_LAUNCH_CHECK();
+  hipLaunchKernelGGL(pose_fc_kernel, dim3(Q, 6), dim3(64), 0, st, means, C, w, b, pose);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+__global__ __launch_bounds__(256) void pose_head_dx_kernel(const float* __restrict__ dpose, int C,
+                                                           long HW, const float* __restrict__ w,
+                                                           float* __restrict__ dx, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long qc = i / HW;
+  const int c = (int)(qc % C);
+  const long q = qc / C;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) s += dpose[q * 6 + k] * w[(long)k * C + c];
+  dx[i] = s * (1e-2f / (float)HW);
+}
+
+__global__ __launch_bounds__(256) void pose_head_dw_kernel(const float* __restrict__ dpose, int Q,
+                                                           int C, const float* __restrict__ means,
+                                                           float* __restrict__ dw,
+                                                           float* __restrict__ db) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx < 6 * C) {
+    const int k = idx / C, c = idx % C;
+    float s = 0.f;
+    for (int q = 0; q < Q; ++q) s += dpose[q * 6 + k] * means[(long)q * C + c];
+    dw[idx] = 1e-2f * s;
+  }
+  if (idx < 6) {
+    float s = 0.f;
+    for (int q = 0; q < Q; ++q) s += dpose[q * 6 + idx];
+    db[idx] = 1e-2f * s;
+  }
+}
+
+int pose_head_bwd(const float* dpose, int Q, int C, long HW, const float* w, const float* means,
+                  float* dx, float* dw, float* db, hipStream_t st) {
+  const long n = (long)Q * C * HW;
+  hipLaunchKernelGGL(pose_head_dx_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dpose, C, HW, w, dx, n);
+  MD2_LAUNCH_CHECK();
+  hipLaunchKernelGGL(pose_head_dw_kernel, dim3(cdiv(6 * C, 256)), dim3(256), 0, st, dpose, Q, C,
+                     means, dw, db);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// elementwise helpers
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void axpy_kernel(float* __restrict__ y, const float* __restrict__ x,
+                                                   long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] += x[i];
+}
+
+int axpy(float* y, const float* x, long n, hipStream_t st) {
+  hipLaunchKernelGGL(axpy_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, y, x, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// pose pairs q = s*N + n read (sq[q], sq[q+N]) (src/model.jl:65-70 in frame-major order):
+// dsq[b] = (b < 2N ? dpin[b][0:C] : 0) + (b >= N ? dpin[b-N][C:2C] : 0)
+__global__ __launch_bounds__(256) void pair_grad_kernel(const float* __restrict__ dpin, int N, int C,
+                                                        long HW, float* __restrict__ dsq, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long per = (long)C * HW;
+  const long b = i / per, r = i - b * per;
+  float s = 0.f;
+  if (b < 2 * N) s += dpin[b * 2 * per + r];
+  if (b >= N) s += dpin[(b - N) * 2 * per + per + r];
+  dsq[i] = s;
+}
+
+int pair_grad_gather(const float* dpin, int N, int C, long HW, float* dsq, hipStream_t st) {
+  const long n = 3L * N * C * HW;
+  hipLaunchKernelGGL(pair_grad_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dpin, N, C, HW, dsq, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// Flux ADAM (Flux.Optimise.apply!): m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+// p -= lr * (m / bc1) / (sqrt(v / bc2) + eps), with bc = 1 - beta^t.
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n,
+                                                   float lr, float b1, float b2, float eps, float bc1,
+                                                   float bc2, float gscale) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i] * gscale;
+  const float mi = b1 * m[i] + (1.f - b1) * gi;
+  const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  p[i] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+}
+
+int adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
+              float eps, float bc1, float bc2, float gscale, hipStream_t st) {
+  hipLaunchKernelGGL(adam_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, p, g, m, v, n, lr, b1, b2,
+                     eps, bc1, bc2, gscale);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+}  // namespace md2

@@ -1,9 +1,14 @@
 """md2hip -- MI355X-native hot path of the Monodepth2.jl training step.
 
 Host-side mirror of the reference's Julia API (``Params``, ``TrainCache``, ``Model``,
-``DepthDecoder``, ``PoseDecoder``, ``train_loss``, ``eval_disparity``) over the C-ABI of
-``libmd2hip.so`` (include/md2.h).  There is no CPU fallback: every op runs the HIP kernels."""
+``ResidualNetwork``, ``DepthDecoder``, ``PoseDecoder``, ``train_loss``, ``eval_disparity``,
+``ADAM``) over the C-ABI of ``libmd2hip.so`` (include/md2.h).  There is no CPU fallback: every
+op runs the HIP kernels and a missing library raises."""
 from ._lib import MD2Error, lib  # noqa: F401
 from .loss import Params, TrainCache, depth10k_intrinsics, loss_tail, pack_poses  # noqa: F401
+from .model import (ADAM, DepthDecoder, Model, Pose, PoseDecoder, ResidualNetwork, ResNet,  # noqa: F401
+                    eval_disparity, gradient, param_table, train_loss, train_step)
 
-__all__ = ["Params", "TrainCache", "depth10k_intrinsics", "loss_tail", "pack_poses", "lib", "MD2Error"]
+__all__ = ["Params", "TrainCache", "depth10k_intrinsics", "loss_tail", "pack_poses", "lib", "MD2Error",
+           "ADAM", "DepthDecoder", "Model", "Pose", "PoseDecoder", "ResidualNetwork", "ResNet",
+           "eval_disparity", "gradient", "param_table", "train_loss", "train_step"]

@@ -44,6 +44,19 @@ class ConvDesc(C.Structure):
                                        "reflect", "act")]
 
 
+class ModelCfg(C.Structure):
+    """``md2_model_cfg``."""
+    _fields_ = [
+        ("arch", C.c_int), ("in_channels", C.c_int), ("batch", C.c_int),
+        ("width", C.c_int), ("height", C.c_int),
+        ("n_levels", C.c_int), ("scale_levels", C.c_int * MAX_SCALES),
+        ("K", C.c_float * 9), ("invK", C.c_float * 9),
+        ("min_depth", C.c_float), ("max_depth", C.c_float), ("disparity_smoothness", C.c_float),
+        ("scales", C.c_float * MAX_SCALES),
+        ("automasking", C.c_int), ("target", C.c_int), ("src0", C.c_int), ("src1", C.c_int),
+    ]
+
+
 _lib = None
 _load_error = None
 
@@ -54,6 +67,7 @@ _SIGS = {
     "md2_abi_version": (C.c_int, []),
     "md2_last_error": (C.c_char_p, []),
     "md2_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "md2_memcpy_d2d": (C.c_int, [P, P, C.c_size_t, P]),
     "md2_loss_workspace_size": (C.c_size_t, [C.POINTER(LossCfg)]),
     "md2_loss_fwd_bwd": (C.c_int, [C.POINTER(LossCfg), FP, P, P, P, C.c_float, C.POINTER(LossOut), P, P]),
     "md2_so3_compose_fwd": (C.c_int, [P, C.c_int, C.c_int, P, P]),
@@ -63,6 +77,21 @@ _SIGS = {
     "md2_conv2d_dgrad": (C.c_int, [C.POINTER(ConvDesc), P, P, P, P, P]),
     "md2_conv2d_wgrad": (C.c_int, [C.POINTER(ConvDesc), P, P, P, P, P, P]),
     "md2_act_backward": (C.c_int, [P, P, P, C.c_longlong, C.c_int, P]),
+    "md2_arch_param_count": (C.c_int, [C.POINTER(ModelCfg), C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
+    "md2_arch_param_info": (C.c_int, [C.POINTER(ModelCfg), C.c_int, C.c_char_p, C.c_int,
+                                      C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_longlong)]),
+    "md2_model_create": (C.c_int, [C.POINTER(ModelCfg), P, P, C.POINTER(C.c_void_p)]),
+    "md2_model_destroy": (C.c_int, [P]),
+    "md2_model_device_bytes": (C.c_size_t, [P]),
+    "md2_model_repack": (C.c_int, [P, P]),
+    "md2_model_forward_loss": (C.c_int, [P, P, P, P, P, P]),
+    "md2_model_num_segments": (C.c_int, [P]),
+    "md2_model_backward_segment": (C.c_int, [P, C.c_int, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong), P]),
+    "md2_model_adam": (C.c_int, [P, P, P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_float, P]),
+    "md2_model_train_step": (C.c_int, [P, P, P, P, P, C.c_float, C.c_int, P, P]),
+    "md2_model_outputs": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                    C.POINTER(C.c_void_p)]),
+    "md2_model_eval_disparity": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_void_p), P]),
 }
 
 

@@ -1,0 +1,326 @@
+"""Host mirror of the reference's model API over libmd2hip.so.
+
+Reference (Julia): ``ResidualNetwork(18; in_channels, classes=nothing)`` (ResNet.jl),
+``DepthDecoder(; encoder_channels, scale_levels, embedding_levels)`` (src/depth_decoder.jl:26),
+``PoseDecoder(encoder_out_channels)`` (src/pose_decoder.jl:13), ``Model(encoder, depth_decoder,
+pose_decoder)`` (src/model.jl:24-29), ``train_loss`` (src/training.jl:21), ``eval_disparity``
+(src/model.jl:63) and the ``gradient(θ)`` / ``update!(ADAM)`` loop (scripts/script.jl:84-86).
+
+The Julia objects are size-agnostic; the HIP executor is planned for one (batch, height, width,
+TrainCache, Params) and cached per such key.  Parameters live in ONE flat fp32 device vector
+(``Model.flat``) in the order of ``md2_arch_param_info``; ``Model.parameters()`` are views."""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import ModelCfg, check, lib, ptr, stream_of
+from .loss import Params, TrainCache, depth10k_intrinsics
+
+
+class ResidualNetwork:
+    """``ResidualNetwork(depth; in_channels, classes=nothing)`` (ext ResNet.jl, torchvision
+    topology).  ``stages`` gives the channel list used by the decoders (scripts/script.jl:78)."""
+
+    def __init__(self, depth: int = 18, *, in_channels: int = 3, classes=None):
+        if depth not in (18, 34, 50):
+            raise ValueError("ResidualNetwork depth must be 18, 34 or 50")
+        if classes is not None:
+            raise NotImplementedError("the classification head is not part of the depth model")
+        self.depth = depth
+        self.in_channels = in_channels
+        self.stages = (64, 64, 128, 256, 512) if depth in (18, 34) else (64, 256, 512, 1024, 2048)
+
+
+ResNet = ResidualNetwork
+
+
+class DepthDecoder:
+    """``DepthDecoder(; encoder_channels, scale_levels, embedding_levels=21)``."""
+
+    def __init__(self, *, encoder_channels, scale_levels, embedding_levels: int = 21):
+        levels = list(scale_levels)
+        if len(levels) > 5 or min(levels) < 1 or max(levels) > 5:   # src/depth_decoder.jl:27-29
+            raise ValueError("`scale_levels` should be at most of length 5 and have values in [1, 5] range.")
+        if embedding_levels != 0:
+            # defects D2/D4: the MPI-embedding decoder is forward-only upstream
+            raise NotImplementedError("the HIP train step runs the mono DepthDecoder (embedding_levels=0)")
+        if levels != sorted(set(levels)) or levels[-1] != 5 or levels[0] < 2:
+            raise NotImplementedError("HIP DepthDecoder supports increasing scale_levels in 2:5 ending at 5")
+        self.encoder_channels = tuple(encoder_channels)
+        self.scale_levels = tuple(levels)
+        self.embedding_levels = embedding_levels
+
+
+class PoseDecoder:
+    """``PoseDecoder(encoder_out_channels)``."""
+
+    def __init__(self, encoder_out_channels: int):
+        self.encoder_out_channels = encoder_out_channels
+
+
+@dataclass
+class Pose:
+    """``Pose{rvec (3,N), tvec (3,1,N)}`` (src/pose_decoder.jl:1-5) as [N,3] tensors."""
+    rvec: object
+    tvec: object
+
+
+def _cfg(arch, in_ch, levels, batch=1, width=64, height=64, cache: Optional[TrainCache] = None,
+         params: Optional[Params] = None) -> ModelCfg:
+    c = ModelCfg()
+    c.arch, c.in_channels, c.batch, c.width, c.height = arch, in_ch, batch, width, height
+    c.n_levels = len(levels)
+    for i, l in enumerate(levels):
+        c.scale_levels[i] = l
+    if cache is not None:
+        K = np.asarray(cache.K, dtype=np.float64).reshape(-1)
+        iK = np.asarray(cache.invK, dtype=np.float64).reshape(-1)
+        for i in range(9):
+            c.K[i], c.invK[i] = float(K[i]), float(iK[i])
+        for i, s in enumerate(cache.scales):
+            c.scales[i] = float(s)
+        if tuple(cache.source_ids) != (1, 3) or cache.target_id != 2:
+            raise NotImplementedError("HIP model supports target_id=2, source_ids=[1,3]")
+        c.target, c.src0, c.src1 = cache.target_id - 1, cache.source_ids[0] - 1, cache.source_ids[1] - 1
+    if params is not None:
+        c.min_depth, c.max_depth = params.min_depth, params.max_depth
+        c.disparity_smoothness = params.disparity_smoothness
+        c.automasking = int(params.automasking)
+    return c
+
+
+def param_table(arch=18, in_channels=3, scale_levels=(2, 3, 4, 5)):
+    """[(name, shape, offset)] of the flat parameter vector (host-only library query)."""
+    cfg = _cfg(arch, in_channels, scale_levels)
+    ne, nel = C.c_longlong(), C.c_longlong()
+    check(lib().md2_arch_param_count(C.byref(cfg), C.byref(ne), C.byref(nel)), "md2_arch_param_count")
+    out = []
+    name = C.create_string_buffer(128)
+    nd, off = C.c_int(), C.c_longlong()
+    shp = (C.c_int * 4)()
+    for i in range(ne.value):
+        check(lib().md2_arch_param_info(C.byref(cfg), i, name, 128, C.byref(nd), shp, C.byref(off)),
+              "md2_arch_param_info")
+        out.append((name.value.decode(), tuple(shp[j] for j in range(nd.value)), off.value))
+    return out, nel.value
+
+
+def flux_init(table, total, seed=42):
+    """Flux defaults (glorot_uniform conv weights, zero bias, BN gamma=1 beta=0) on the host,
+    float64 -> the caller casts.  Identical to oracle.init_params for the same seed."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    flat = torch.empty(total, dtype=torch.float64)
+    for name, shape, off in table:
+        n = int(np.prod(shape))
+        if name.endswith(".weight"):
+            cout, cin, kh, kw = shape
+            lim = math.sqrt(6.0 / (cin * kh * kw + cout * kh * kw))
+            v = (torch.rand(shape, generator=g, dtype=torch.float64) * 2 - 1) * lim
+        elif name.endswith(".gamma"):
+            v = torch.ones(n, dtype=torch.float64)
+        else:
+            v = torch.zeros(n, dtype=torch.float64)
+        flat[off:off + n] = v.reshape(-1)
+    return flat
+
+
+class _Executor:
+    """One libmd2hip model instance (activations/workspace) for a fixed problem size."""
+
+    def __init__(self, model: "Model", batch, height, width, cache: TrainCache, params: Params):
+        self.model = model
+        self.batch, self.height, self.width = batch, height, width
+        cfg = _cfg(model.encoder.depth, model.encoder.in_channels, model.depth_decoder.scale_levels,
+                   batch, width, height, cache, params)
+        h = C.c_void_p()
+        check(lib().md2_model_create(C.byref(cfg), ptr(model.flat), ptr(model.grad), C.byref(h)),
+              "md2_model_create")
+        self.handle = h
+        self.nseg = lib().md2_model_num_segments(h)
+        self.automask = params.automasking
+        self.forwarded = False
+        check(lib().md2_model_repack(h, stream_of(model.device)), "md2_model_repack")
+
+    def __del__(self):
+        try:
+            if self.handle:
+                lib().md2_model_destroy(self.handle)
+        except Exception:
+            pass
+
+    def device_bytes(self):
+        return lib().md2_model_device_bytes(self.handle)
+
+    def forward_loss(self, x, auto_loss=None, loss=None, terms=None):
+        import torch
+        loss = loss if loss is not None else torch.empty(1, dtype=torch.float32, device=x.device)
+        am = auto_loss.contiguous() if (self.automask and auto_loss is not None) else None
+        check(lib().md2_model_forward_loss(self.handle, ptr(x), ptr(am), ptr(loss), ptr(terms),
+                                           stream_of(x.device)), "md2_model_forward_loss")
+        self.forwarded = True
+        return loss
+
+    def backward_segment(self, k):
+        off, ln = C.c_longlong(), C.c_longlong()
+        check(lib().md2_model_backward_segment(self.handle, k, C.byref(off), C.byref(ln),
+                                               stream_of(self.model.device)), "md2_model_backward_segment")
+        return off.value, ln.value
+
+    def backward(self):
+        return [self.backward_segment(k) for k in range(self.nseg)]
+
+    def outputs(self):
+        """(disparities [N,1,h,w] views, poses [2N,6] view) of the last forward (device memory
+        owned by the executor; clone to keep)."""
+        import torch
+        nl = len(self.model.depth_decoder.scale_levels)
+        dptr = (C.c_void_p * 5)()
+        w = (C.c_int * 5)()
+        h = (C.c_int * 5)()
+        pp = C.c_void_p()
+        check(lib().md2_model_outputs(self.handle, dptr, w, h, C.byref(pp)), "md2_model_outputs")
+        disps = [_wrap(dptr[i], (self.batch, 1, h[i], w[i]), self.model.device) for i in range(nl)]
+        pose = _wrap(pp.value, (2 * self.batch, 6), self.model.device)
+        return disps, pose
+
+
+def _wrap(p, shape, device):
+    """Copy library-owned device memory into a fresh torch tensor (md2_memcpy_d2d)."""
+    import torch
+    n = int(np.prod(shape))
+    out = torch.empty(shape, dtype=torch.float32, device=device)
+    check(lib().md2_memcpy_d2d(ptr(out), C.c_void_p(p), n * 4, stream_of(device)), "md2_memcpy_d2d")
+    return out
+
+
+class Model:
+    """``Model(encoder, depth_decoder, pose_decoder)`` (src/model.jl:24-29)."""
+
+    def __init__(self, encoder: ResidualNetwork, depth_decoder: DepthDecoder,
+                 pose_decoder: PoseDecoder, *, device="cuda", seed: int = 42):
+        import torch
+        if tuple(depth_decoder.encoder_channels) != tuple(encoder.stages):
+            raise ValueError("DepthDecoder encoder_channels must equal encoder.stages")
+        if pose_decoder.encoder_out_channels != encoder.stages[-1]:
+            raise ValueError("PoseDecoder channels must equal encoder.stages[end]")
+        self.encoder, self.depth_decoder, self.pose_decoder = encoder, depth_decoder, pose_decoder
+        self.device = torch.device(device)
+        self.table, self.numel = param_table(encoder.depth, encoder.in_channels, depth_decoder.scale_levels)
+        self.flat = flux_init(self.table, self.numel, seed).to(self.device, torch.float32)
+        self.grad = torch.zeros_like(self.flat)
+        self._ex: Dict[tuple, _Executor] = {}
+
+    # -- parameters (Flux.params(model)) ----------------------------------------------------
+    def parameters(self) -> Dict[str, object]:
+        return {name: self.flat[off:off + int(np.prod(shape))].view(shape) for name, shape, off in self.table}
+
+    def load_flat(self, flat):
+        self.flat.copy_(flat.to(self.flat.device, self.flat.dtype))
+        for ex in self._ex.values():
+            check(lib().md2_model_repack(ex.handle, stream_of(self.device)), "md2_model_repack")
+
+    def executor(self, x_shape, cache: TrainCache, params: Params) -> _Executor:
+        N, L, Cc, H, W = x_shape
+        if L != 3 or Cc != self.encoder.in_channels:
+            raise ValueError("x must be [N, 3, in_channels, H, W]")
+        if (W, H) != tuple(params.target_size):
+            raise ValueError("x size != Params.target_size")
+        key = (N, H, W, tuple(np.asarray(cache.K).reshape(-1)), tuple(cache.scales), params.min_depth,
+               params.max_depth, params.disparity_smoothness, params.automasking)
+        if key not in self._ex:
+            self._ex[key] = _Executor(self, N, H, W, cache, params)
+        self._last = self._ex[key]
+        return self._last
+
+    def __call__(self, x, source_ids=(1, 3), target_id=2, cache: Optional[TrainCache] = None,
+                 params: Optional[Params] = None):
+        """Mono-mode forward (src/model.jl:31-55): returns (disparities, [Pose, Pose])."""
+        N, L, Cc, H, W = x.shape
+        if cache is None:
+            K, iK = depth10k_intrinsics(W, H)
+            cache = TrainCache(K=K, invK=iK, target_id=target_id, source_ids=tuple(source_ids))
+        if params is None:
+            params = Params(target_size=(W, H), batch_size=N, automasking=False)
+        ex = self.executor(tuple(x.shape), cache, params)
+        ex.forward_loss(x, None)
+        disps, pose = ex.outputs()
+        return disps, [Pose(pose[s * N:(s + 1) * N, 0:3], pose[s * N:(s + 1) * N, 3:6]) for s in range(2)]
+
+
+def train_loss(model: Model, x, auto_loss, cache: TrainCache, params: Params,
+               do_visualization: bool = False):
+    """``train_loss(model, x, auto_loss, cache, params, do_visualization)`` (src/training.jl:21).
+    Runs the forward and the fused loss-tail pullback; call ``gradient(model)`` for the rest of
+    the backward.  Returns (loss, vis_disparity, vis_warped, vis_loss)."""
+    ex = model.executor(tuple(x.shape), cache, params)
+    loss = ex.forward_loss(x, auto_loss)
+    vis_disparity = None
+    if do_visualization:
+        vis_disparity = ex.outputs()[0][-1].cpu()
+    return loss, vis_disparity, None, None
+
+
+def gradient(model: Model):
+    """Backward of the last ``train_loss`` (Zygote ``gradient(θ)``): fills ``model.grad``."""
+    ex = model._last
+    if not ex.forwarded:
+        raise RuntimeError("gradient() needs a preceding train_loss()")
+    ex.backward()
+    return model.grad
+
+
+class ADAM:
+    """Flux ``ADAM(eta, (beta1, beta2))`` with eps = 1e-8 (scripts/script.jl:85)."""
+
+    def __init__(self, eta=1e-3, beta=(0.9, 0.999), eps=1e-8):
+        self.eta, self.beta, self.eps = eta, beta, eps
+        self.t = 0
+        self.m = self.v = None
+
+    def update(self, model: Model, grad_scale: float = 1.0):
+        """``Flux.Optimise.update!(opt, θ, ∇)`` on the flat vector (in place)."""
+        import torch
+        if self.m is None:
+            self.m = torch.zeros_like(model.flat)
+            self.v = torch.zeros_like(model.flat)
+        self.t += 1
+        check(lib().md2_model_adam(model._last.handle, ptr(self.m), ptr(self.v), self.eta, self.beta[0],
+                                   self.beta[1], self.eps, self.t, grad_scale, stream_of(model.device)),
+              "md2_model_adam")
+
+
+def train_step(model: Model, x, auto_loss, cache: TrainCache, params: Params, opt: ADAM):
+    """One ``gradient(θ) do train_loss(...)[1] end`` + ``update!`` on one GPU."""
+    loss, *_ = train_loss(model, x, auto_loss, cache, params)
+    gradient(model)
+    opt.update(model)
+    return loss
+
+
+def eval_disparity(model: Model, x, cache: Optional[TrainCache] = None):
+    """``eval_disparity(m, x)`` (src/model.jl:63) for x [N, C, H, W] (train-mode BatchNorm, as
+    the reference never calls testmode!).  Uses an executor of batch >= N."""
+    N, Cc, H, W = x.shape
+    if cache is None:
+        K, iK = depth10k_intrinsics(W, H)
+        cache = TrainCache(K=K, invK=iK)
+    params = Params(target_size=(W, H), batch_size=N, automasking=False)
+    ex = model.executor((N, 3, Cc, H, W), cache, params)
+    dptr = (C.c_void_p * 5)()
+    check(lib().md2_model_eval_disparity(ex.handle, ptr(x), N, dptr, stream_of(x.device)),
+          "md2_model_eval_disparity")
+    out = []
+    h, w = H, W
+    nl = len(model.depth_decoder.scale_levels)
+    shapes = []
+    for l in model.depth_decoder.scale_levels:
+        f = 2 ** (5 - l)
+        shapes.append((N, 1, H // f, W // f))
+    return [_wrap(dptr[i], shapes[i], x.device) for i in range(nl)]

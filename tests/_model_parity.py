@@ -1,0 +1,75 @@
+"""Full train-step parity helper: GPU Model (libmd2hip) vs the fp64 CPU oracle on the same
+flat parameters and inputs, with the GPU's per-pixel argmin imposed on the oracle."""
+import torch
+
+import md2hip
+from oracle import md2_oracle as O
+from tests import _data as D
+
+
+def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7):
+    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
+    K, invK = D.intrinsics(W, H)
+    enc = md2hip.ResNet(arch, in_channels=C)
+    model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
+                                                  embedding_levels=0),
+                         md2hip.PoseDecoder(enc.stages[-1]), seed=42)
+    cache = md2hip.TrainCache(K=K.numpy(), invK=invK.numpy())
+    params = md2hip.Params(target_size=(W, H), batch_size=N, automasking=False)
+    xg = x.float().cuda().contiguous()
+    loss, *_ = md2hip.train_loss(model, xg, None, cache, params)
+    disps, pose = model._last.outputs()
+    md2hip.gradient(model)
+    poses_g = [(pose[:N, :3].contiguous(), pose[:N, 3:].contiguous()),
+               (pose[N:, :3].contiguous(), pose[N:, 3:].contiguous())]
+    tail = md2hip.loss_tail([d.contiguous() for d in disps], poses_g, xg, None, cache, params, visualize=True)
+    torch.cuda.synchronize()
+    g = {"loss": loss.item(), "tail_loss": tail["loss"].item(), "disps": [d.cpu() for d in disps],
+         "pose": pose.cpu(), "grad": model.grad.cpu(), "sel": tail["vis_sel"].cpu()}
+    spec = O.param_spec(arch, C, (2, 3, 4, 5))
+    flat = model.flat.detach().double().cpu().clone().requires_grad_(True)
+    P = O.unflatten(flat, spec)
+    d_o, p_o = O.model_forward(P, x, arch=arch)
+    cache_o = O.TrainCache(K=K, invK=invK)
+    par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
+    forced = [g["sel"][s].unsqueeze(1).long() for s in range(4)]
+    loss_o = O.loss_from_outputs(d_o, p_o, x, None, cache_o, par_o, forced_sel=forced)
+    loss_o.backward()
+    o = {"loss": loss_o.item(), "disps": [d.detach() for d in d_o],
+         "pose": torch.cat([torch.cat([r, t], 1) for r, t in p_o], 0).detach(), "grad": flat.grad}
+    errs = {}
+    for name, shape, off in [(n, s, None) for n, s in spec]:
+        pass
+    off = 0
+    for name, shape in spec:
+        n = 1
+        for s in shape:
+            n *= s
+        errs[name] = D.rel_err(g["grad"][off:off + n], o["grad"][off:off + n])
+        off += n
+    return g, o, errs
+
+
+def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=None, sel=None):
+    """Per-tensor gradient error of the SAME oracle run in fp32 vs fp64 (the fp32 noise floor)."""
+    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
+    K, invK = D.intrinsics(W, H)
+    spec = O.param_spec(arch, C, (2, 3, 4, 5))
+    grads = []
+    for dt in (torch.float64, torch.float32):
+        f = flat.to(dt).clone().requires_grad_(True)
+        P = O.unflatten(f, spec)
+        d_o, p_o = O.model_forward(P, x.to(dt), arch=arch)
+        cache_o = O.TrainCache(K=K.to(dt), invK=invK.to(dt))
+        par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
+        forced = [s.unsqueeze(1).long() for s in sel]
+        O.loss_from_outputs(d_o, p_o, x.to(dt), None, cache_o, par_o, forced_sel=forced).backward()
+        grads.append(f.grad.double())
+    errs, off = {}, 0
+    for name, shape in spec:
+        n = 1
+        for s in shape:
+            n *= s
+        errs[name] = D.rel_err(grads[1][off:off + n], grads[0][off:off + n])
+        off += n
+    return errs

@@ -1,0 +1,13 @@
+import os, sys
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, R); sys.path.insert(0, os.path.join(R, "monodepth2.jl_amd"))
+import torch
+from tests import _data as D
+from tests._model_parity import run
+for strict in (True, False):
+    g, o, errs = run(strict=strict)
+    print("strict", strict, "loss", g["loss"], g["tail_loss"], o["loss"])
+    print(" disp rel", [D.rel_err(a, b) for a, b in zip(g["disps"], o["disps"])], "pose rel", D.rel_err(g["pose"], o["pose"]))
+    print(" total grad rel", D.rel_err(g["grad"], o["grad"]))
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:12]
+    for k, v in worst: print(f"   {k:40s} {v:.3e}")
