@@ -291,6 +291,16 @@ int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, f
   return model_adam(m->impl, adam_m, adam_v, lr, 0.9f, 0.999f, 1e-8f, step, 1.f, st);
 }
 
+int md2_model_set_profiling(md2_model* m, int on) {
+  MD2_CHECK_ARG(m, "model");
+  return model_set_profiling(m->impl, on);
+}
+
+int md2_model_profile_read(md2_model* m, double* out, int ncat) {
+  MD2_CHECK_ARG(m, "model");
+  return model_profile_read(m->impl, out, ncat);
+}
+
 int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose) {
   MD2_CHECK_ARG(m, "model");
   return model_outputs(m->impl, disp, w, h, pose);

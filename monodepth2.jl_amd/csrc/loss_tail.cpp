@@ -109,7 +109,9 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     pa.loss_map = o.vis_loss ? o.vis_loss + s * plane : nullptr;
     pa.sel_map = o.vis_sel ? o.vis_sel + s * plane : nullptr;
     pa.N = c.N;
+    if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[2 * s], st));
     MD2_TRY(launch_photometric(pa, g, c.C, st));
+    if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[2 * s + 1], st));
 
     SmoothArgs sa{};
     sa.disp = disp[s];

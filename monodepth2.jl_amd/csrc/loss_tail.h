@@ -31,6 +31,7 @@ struct LossTailOut {
   float* d_pose;
   float* vis_loss;
   signed char* vis_sel;
+  hipEvent_t* photo_events = nullptr;   // optional [2*nscales] around each photometric launch
 };
 
 // disp[s]: [N][dh][dw] sigmoid outputs; pose: [2N][6] (rvec, tvec) per (source, sample);

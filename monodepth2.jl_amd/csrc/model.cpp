@@ -183,6 +183,7 @@ struct RConv {
   ConvShape s{};          // N filled per call
   float* wpf = nullptr;   // packed forward weights
   float* wpd = nullptr;   // packed dgrad weights
+  int cat = PROF_CONV_OTHER;
 };
 struct RBN {
   PBN p;
@@ -352,6 +353,7 @@ class Model {
         for (size_t k = 0; k < bs.convs.size(); ++k) {
           EncStage es;
           MD2_TRY(make_conv(es.conv, bs.convs[k], h, w, true, wsn));
+          es.conv.cat = bs.convs[k].k == 3 ? PROF_CONV3_ENC : PROF_CONV_OTHER;
           need_ws(es.conv, B, wsn, true);
           MD2_TRY(make_bn(es.bn, bs.bns[k]));
           h = es.conv.s.Ho;
@@ -496,6 +498,40 @@ class Model {
   }
 
   // -------------------------------------------------------------------------------------------
+  // ---- optional HIP-event profiling of the hot kernels (bench.py roofline) ----------------
+  struct ProfRec {
+    hipEvent_t a, b;
+    int cat;
+    double work;
+  };
+  bool prof = false;
+  std::vector<ProfRec> recs;
+  std::vector<hipEvent_t> evpool;
+  size_t evi = 0;
+  hipEvent_t ev() {
+    if (evi == evpool.size()) {
+      hipEvent_t e;
+      (void)hipEventCreate(&e);
+      evpool.push_back(e);
+    }
+    return evpool[evi++];
+  }
+  hipEvent_t prof_begin(hipStream_t st) {
+    if (!prof) return nullptr;
+    hipEvent_t e = ev();
+    (void)hipEventRecord(e, st);
+    return e;
+  }
+  void prof_end(hipEvent_t a, int cat, double work, hipStream_t st) {
+    if (!prof) return;
+    hipEvent_t b = ev();
+    (void)hipEventRecord(b, st);
+    recs.push_back({a, b, cat, work});
+  }
+  static double conv_flops(const ConvShape& s) {
+    return 2.0 * s.N * (double)s.Ho * s.Wo * s.Cout * s.Cin * s.KH * s.KW;
+  }
+
   int conv_f(RConv& c, int nimg, const TensorIn& in, float* out, long out_bs, int act,
              int accumulate, hipStream_t st) {
     ConvShape s = c.s;
@@ -506,7 +542,10 @@ class Model {
     o.bias = P(c.p.b);
     o.act = act;
     o.accumulate = accumulate;
-    return conv_fwd(s, in, c.wpf, o, cws, st);
+    hipEvent_t e = prof_begin(st);
+    MD2_TRY(conv_fwd(s, in, c.wpf, o, cws, st));
+    prof_end(e, c.cat, conv_flops(s), st);
+    return MD2_OK;
   }
   static TensorIn tin(const float* p, int C, long HW) {
     TensorIn t;
@@ -651,14 +690,45 @@ class Model {
     o.loss = loss ? loss : loss_buf;
     o.terms = terms;
     o.d_pose = d_pose;
-    return loss_tail_run(tail, disps, pose, x, cfg.automask ? automask : nullptr, 1.f, o, tail_ws, st);
+    hipEvent_t pev[2 * MAX_SCALES] = {};
+    if (prof) {
+      for (int k = 0; k < 2 * tail.nscales; ++k) pev[k] = ev();
+      o.photo_events = pev;
+    }
+    MD2_TRY(loss_tail_run(tail, disps, pose, x, cfg.automask ? automask : nullptr, 1.f, o, tail_ws, st));
+    if (prof) {
+      // algorithmic bytes per pixel and scale: disparity 4 + target 4C + two sources 8C + d_disp 4
+      const double bytes = (double)N * cfg.H * cfg.W * (8.0 + 12.0 * cfg.arch.in_ch);
+      for (int k = 0; k < tail.nscales; ++k) recs.push_back({pev[2 * k], pev[2 * k + 1], PROF_PHOTO, bytes});
+    }
+    return MD2_OK;
+  }
+
+  int profile_read(double* out, int ncat) {
+    for (int c = 0; c < ncat * 3; ++c) out[c] = 0.0;
+    for (auto& r : recs) {
+      MD2_HIP(hipEventSynchronize(r.b));
+      float ms = 0.f;
+      MD2_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+      if (r.cat < ncat) {
+        out[r.cat * 3 + 0] += ms;
+        out[r.cat * 3 + 1] += r.work;
+        out[r.cat * 3 + 2] += 1.0;
+      }
+    }
+    recs.clear();
+    evi = 0;
+    return MD2_OK;
   }
 
   // -------------------------------------------------------------------------------------------
   int conv_w(RConv& c, int nimg, const TensorIn& in, const float* dy, hipStream_t st) {
     ConvShape s = c.s;
     s.N = nimg;
-    return conv_wgrad(s, in, dy, grads + c.p.w, Gd(c.p.b), 0, cws, st);
+    hipEvent_t e = prof_begin(st);
+    MD2_TRY(conv_wgrad(s, in, dy, grads + c.p.w, Gd(c.p.b), 0, cws, st));
+    prof_end(e, c.cat, conv_flops(s), st);
+    return MD2_OK;
   }
   int conv_d(RConv& c, int nimg, const float* dy, float* dx, long dx_bs, int acc, hipStream_t st,
              float* dx1 = nullptr, long dx1_bs = 0, int c0 = 1 << 30) {
@@ -671,7 +741,10 @@ class Model {
     o.bs1 = dx1_bs;
     o.c0 = c0;
     o.accumulate = acc;
-    return conv_dgrad(s, dy, c.wpd, o, cws, st);
+    hipEvent_t e = prof_begin(st);
+    MD2_TRY(conv_dgrad(s, dy, c.wpd, o, cws, st));
+    prof_end(e, c.cat, conv_flops(s), st);
+    return MD2_OK;
   }
   int bn_bwd(RBN& bn, const float* dout, const float* mask, const float* y, int nimg, long HW,
              float* dy, float* dres, int dres_acc, hipStream_t st) {
@@ -904,6 +977,19 @@ int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipS
       if (d.head >= 0) disp_out[li++] = d.disp;
   }
   return MD2_OK;
+}
+
+int model_set_profiling(Model* m, int on) {
+  MD2_CHECK_ARG(m, "model");
+  m->prof = on != 0;
+  m->recs.clear();
+  m->evi = 0;
+  return MD2_OK;
+}
+
+int model_profile_read(Model* m, double* out, int ncat) {
+  MD2_CHECK_ARG(m && out && ncat > 0, "profile_read args");
+  return m->profile_read(out, ncat);
 }
 
 long model_param_count(Model* m) { return m ? m->spec.total : 0; }

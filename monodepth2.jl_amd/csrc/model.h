@@ -39,7 +39,13 @@ struct ModelCfg {
   int target = 1, src0 = 0, src1 = 2;   // 0-based frame ids, L = 3
 };
 
+// profiling categories (HIP events around each launch, md2_model_profile_read)
+enum ProfCat : int { PROF_CONV3_ENC = 0, PROF_CONV_OTHER = 1, PROF_PHOTO = 2, PROF_NCAT = 3 };
+
 class Model;
+int model_set_profiling(Model* m, int on);
+// out[cat*3 + {0,1,2}] = {total ms, total algorithmic work (FLOP or bytes), launches}
+int model_profile_read(Model* m, double* out, int ncat);
 int model_create(const ModelCfg& cfg, float* params, float* grads, Model** out);
 void model_destroy(Model* m);
 

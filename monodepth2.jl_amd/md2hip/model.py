@@ -158,6 +158,18 @@ class _Executor:
     def device_bytes(self):
         return lib().md2_model_device_bytes(self.handle)
 
+    PROF_CATS = ("conv3x3_encoder", "conv_other", "photometric")
+
+    def set_profiling(self, on: bool):
+        check(lib().md2_model_set_profiling(self.handle, int(on)), "md2_model_set_profiling")
+
+    def profile_read(self):
+        """{category: (ms, work, launches)} from HIP events recorded on the model's stream."""
+        n = len(self.PROF_CATS)
+        buf = (C.c_double * (3 * n))()
+        check(lib().md2_model_profile_read(self.handle, buf, n), "md2_model_profile_read")
+        return {c: (buf[3 * i], buf[3 * i + 1], int(buf[3 * i + 2])) for i, c in enumerate(self.PROF_CATS)}
+
     def forward_loss(self, x, auto_loss=None, loss=None, terms=None):
         import torch
         loss = loss if loss is not None else torch.empty(1, dtype=torch.float32, device=x.device)
