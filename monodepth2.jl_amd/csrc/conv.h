@@ -52,6 +52,18 @@ size_t conv_dgrad_packed_elems(const ConvShape& s);
 int conv_pack_fwd(const ConvShape& s, const float* w, float* packed, hipStream_t st);
 int conv_pack_dgrad(const ConvShape& s, const float* w, float* packed, hipStream_t st);
 
+// all packs of a model in ONE launch: a device-resident job table (blocks of 256 elements)
+struct PackJob {
+  const float* w;
+  float* out;
+  int mode;            // 0 forward, 1 dgrad
+  int Cout, Cin, KK, Kpad, Mpad;
+  long block_begin;    // first 256-element block of this job in the batched grid
+};
+PackJob conv_pack_job(const ConvShape& s, int mode, const float* w, float* out);
+long conv_pack_job_blocks(const PackJob& j);
+int conv_pack_batch(const PackJob* dev_jobs, int njobs, long total_blocks, hipStream_t st);
+
 // workspace needed for split-K slabs (bytes)
 size_t conv_fwd_workspace(const ConvShape& s);
 size_t conv_dgrad_workspace(const ConvShape& s);

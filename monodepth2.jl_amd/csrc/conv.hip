@@ -88,6 +88,62 @@ int conv_pack_dgrad(const ConvShape& s, const float* w, float* packed, hipStream
   return MD2_OK;
 }
 
+PackJob conv_pack_job(const ConvShape& s, int mode, const float* w, float* out) {
+  PackJob j{};
+  j.w = w;
+  j.out = out;
+  j.mode = mode;
+  j.Cout = s.Cout;
+  j.Cin = s.Cin;
+  j.KK = s.KH * s.KW;
+  if (mode == 0) {
+    j.Kpad = (int)round_up((long)s.Cin * j.KK, KPAD);
+    j.Mpad = (int)round_up(s.Cout, MPAD);
+  } else {
+    j.Kpad = (int)round_up((long)s.Cout * j.KK, KPAD);
+    j.Mpad = (int)round_up(s.Cin, MPAD);
+  }
+  return j;
+}
+
+long conv_pack_job_blocks(const PackJob& j) { return cdiv((long)j.Kpad * j.Mpad, 256); }
+
+__global__ __launch_bounds__(256) void pack_batch_kernel(const PackJob* __restrict__ jobs, int njobs) {
+  // find the job of this block (jobs sorted by block_begin; few dozen entries)
+  __shared__ int s_job;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].block_begin <= (long)blockIdx.x) lo = mid; else hi = mid - 1;
+    }
+    s_job = lo;
+  }
+  __syncthreads();
+  const PackJob j = jobs[s_job];
+  const long idx = ((long)blockIdx.x - j.block_begin) * 256 + threadIdx.x;
+  if (idx >= (long)j.Kpad * j.Mpad) return;
+  const int k = (int)(idx / j.Mpad), m = (int)(idx % j.Mpad);
+  float v = 0.f;
+  if (j.mode == 0) {
+    const int K = j.Cin * j.KK;
+    if (k < K && m < j.Cout) v = j.w[(long)m * K + k];
+  } else {
+    if (k < j.Cout * j.KK && m < j.Cin) {
+      const int co = k / j.KK, r = k % j.KK;
+      v = j.w[((long)co * j.Cin + m) * j.KK + r];
+    }
+  }
+  j.out[idx] = v;
+}
+
+int conv_pack_batch(const PackJob* dev_jobs, int njobs, long total_blocks, hipStream_t st) {
+  if (njobs == 0) return MD2_OK;
+  hipLaunchKernelGGL(pack_batch_kernel, dim3(total_blocks), dim3(256), 0, st, dev_jobs, njobs);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // kernel arguments
 // ---------------------------------------------------------------------------------------------
@@ -452,38 +508,71 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void splitk_reduce_w_kernel(const float* __restrict__ slab,
-                                                              int splits, long total,
-                                                              float* __restrict__ dw, int acc) {
+// split-K slab reduction for wgrad, two stages for parallelism: stage 1 sums split groups
+// (group g takes splits g, g+G, ...) into part[G][total]; stage 2 sums the G partials.
+constexpr int WRED_GROUPS = 32;
+
+__global__ __launch_bounds__(256) void splitk_reduce_w1_kernel(const float* __restrict__ slab,
+                                                               int splits, long total, int G,
+                                                               float* __restrict__ part) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int g = blockIdx.y;
+  float v0 = 0.f, v1 = 0.f;
+  int s = g;
+  for (; s + G < splits; s += 2 * G) {
+    v0 += slab[(long)s * total + idx];
+    v1 += slab[(long)(s + G) * total + idx];
+  }
+  if (s < splits) v0 += slab[(long)s * total + idx];
+  part[(long)g * total + idx] = v0 + v1;
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_w2_kernel(const float* __restrict__ part,
+                                                               int G, long total,
+                                                               float* __restrict__ dw, int acc) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
   float v = 0.f;
-  for (int s = 0; s < splits; ++s) v += slab[(long)s * total + idx];
+  for (int g = 0; g < G; ++g) v += part[(long)g * total + idx];
   if (acc)
     dw[idx] += v;
   else
     dw[idx] = v;
 }
 
-// bias gradient: db[c] = sum over images and pixels of dY[img][c][:]  (one block per channel)
-__global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict__ dy, int N,
-                                                        int C, long HW, float* __restrict__ db,
-                                                        int acc) {
+// bias gradient db[c] = sum over images and pixels of dY[img][c][:], two stages:
+// grid (C, parts) partial sums over contiguous slices of the N*HW elements, then per channel.
+__global__ __launch_bounds__(256) void bias_grad_partial_kernel(const float* __restrict__ dy, int C,
+                                                                long HW, long total, int parts,
+                                                                float* __restrict__ part) {
   __shared__ float red[4];
-  const int c = blockIdx.x;
+  const int c = blockIdx.x, p = blockIdx.y;
+  const long beg = total * p / parts, end = total * (p + 1) / parts;
   float s = 0.f;
-  for (int img = 0; img < N; ++img) {
-    const float* p = dy + ((long)img * C + c) * HW;
-    for (long i = threadIdx.x; i < HW; i += 256) s += p[i];
+  for (long e = beg + threadIdx.x; e < end; e += 256) {
+    const long img = e / HW, pix = e - img * HW;
+    s += dy[(img * C + c) * HW + pix];
   }
   float v[1] = {s};
   block_sum256<1>(v, red);
-  if (threadIdx.x == 0) {
-    if (acc)
-      db[c] += v[0];
-    else
-      db[c] = v[0];
-  }
+  if (threadIdx.x == 0) part[(long)c * parts + p] = v[0];
+}
+
+__global__ void bias_grad_final_kernel(const float* __restrict__ part, int C, int parts,
+                                       float* __restrict__ db, int acc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int p = 0; p < parts; ++p) s += part[(long)c * parts + p];
+  if (acc)
+    db[c] += s;
+  else
+    db[c] = s;
+}
+
+static int bias_parts(int C, long total) {
+  return (int)std::max(1L, std::min((long)std::max(1, 1024 / C), total / 4096 + 1));
 }
 
 __global__ __launch_bounds__(256) void act_backward_kernel(const float* __restrict__ out,
@@ -541,7 +630,7 @@ Plan plan_w(int M, long N, long K) {
   Plan p{};
   p.BM = 64; p.BN = 128; p.BK = 32;
   const long tiles = (long)cdiv(M, p.BM) * cdiv(N, p.BN);
-  long splits = std::max(1L, (long)TARGET_BLOCKS / tiles);
+  long splits = std::max(1L, (long)512 / tiles);   // 2 blocks/CU resident (191 VGPR+AGPR)
   splits = std::min(splits, std::max(1L, K / (8 * p.BK)));
   p.kper = (int)round_up((K + splits - 1) / splits, p.BK);
   p.splits = (int)((K + p.kper - 1) / p.kper);
@@ -629,7 +718,9 @@ size_t conv_wgrad_workspace(const ConvShape& s) {
   const long K = (long)s.N * s.Ho * s.Wo;
   const long Nc = (long)s.Cin * s.KH * s.KW;
   const Plan p = plan_w(s.Cout, Nc, K);
-  return (size_t)p.splits * s.Cout * Nc * sizeof(float);
+  const size_t groups = (size_t)std::min(p.splits, WRED_GROUPS);
+  return ((size_t)p.splits + groups) * s.Cout * Nc * sizeof(float) +
+         (size_t)s.Cout * bias_parts(s.Cout, K) * sizeof(float) + 256;
 }
 
 int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const TensorOut& y,
@@ -691,9 +782,13 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
   a.dy = dy;
   const Plan p = plan_w(a.g.M, a.g.N, Kpix);
   a.g.kper = p.kper;
-  const size_t need = (size_t)p.splits * a.g.M * a.g.N * sizeof(float);
+  const size_t need = conv_wgrad_workspace(s);
   MD2_CHECK_ARG(ws.ptr && ws.bytes >= need, "conv_wgrad workspace too small");
   a.slab = (float*)ws.ptr;
+  const long total = (long)a.g.M * a.g.N;
+  const int groups = std::min(p.splits, WRED_GROUPS);
+  float* part = a.slab + (long)p.splits * total;
+  float* bpart = part + (long)groups * total;
   dim3 grid(cdiv(a.g.N, p.BN), cdiv(a.g.M, p.BM), p.splits);
   bool launched = false;
 #define MD2_W_CASE(KS, SS, RR)                                                                     \
@@ -709,13 +804,24 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
     return MD2_ENOTSUP;
   }
   MD2_LAUNCH_CHECK();
-  const long total = (long)a.g.M * a.g.N;
-  hipLaunchKernelGGL(splitk_reduce_w_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a.slab,
-                     p.splits, total, dw, accumulate);
+  if (groups > 1) {
+    hipLaunchKernelGGL(splitk_reduce_w1_kernel, dim3(cdiv(total, 256), groups), dim3(256), 0, st,
+                       a.slab, p.splits, total, groups, part);
+    MD2_LAUNCH_CHECK();
+    hipLaunchKernelGGL(splitk_reduce_w2_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, part,
+                       groups, total, dw, accumulate);
+  } else {
+    hipLaunchKernelGGL(splitk_reduce_w2_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a.slab,
+                       1, total, dw, accumulate);
+  }
   MD2_LAUNCH_CHECK();
   if (db) {
-    hipLaunchKernelGGL(bias_grad_kernel, dim3(s.Cout), dim3(256), 0, st, dy, s.N, s.Cout,
-                       (long)s.Ho * s.Wo, db, accumulate);
+    const int parts = bias_parts(s.Cout, Kpix);
+    hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(s.Cout, parts), dim3(256), 0, st, dy, s.Cout,
+                       (long)s.Ho * s.Wo, Kpix, parts, bpart);
+    MD2_LAUNCH_CHECK();
+    hipLaunchKernelGGL(bias_grad_final_kernel, dim3(cdiv(s.Cout, 64)), dim3(64), 0, st, bpart,
+                       s.Cout, parts, db, accumulate);
     MD2_LAUNCH_CHECK();
   }
   return MD2_OK;

@@ -494,7 +494,7 @@ class Model {
       tail_ws = q;
     }
     MD2_TRY(alloc(&loss_buf, 16));
-    return MD2_OK;
+    return build_pack_table();
   }
 
   // -------------------------------------------------------------------------------------------
@@ -555,28 +555,47 @@ class Model {
     return t;
   }
 
-  int repack(hipStream_t st) {
-    auto pk = [&](RConv& c) -> int {
-      MD2_TRY(conv_pack_fwd(c.s, params + c.p.w, c.wpf, st));
-      if (c.wpd) MD2_TRY(conv_pack_dgrad(c.s, params + c.p.w, c.wpd, st));
-      return MD2_OK;
+  // one batched launch re-packs every conv weight (forward and dgrad layouts) after an update
+  PackJob* pack_jobs = nullptr;
+  int pack_njobs = 0;
+  long pack_blocks = 0;
+
+  int build_pack_table() {
+    std::vector<PackJob> jobs;
+    auto pk = [&](RConv& c) {
+      jobs.push_back(conv_pack_job(c.s, 0, params + c.p.w, c.wpf));
+      if (c.wpd) jobs.push_back(conv_pack_job(c.s, 1, params + c.p.w, c.wpd));
     };
-    MD2_TRY(pk(stem));
+    pk(stem);
     for (auto& sg : stages)
       for (auto& b : sg) {
-        for (auto& e : b.st) MD2_TRY(pk(e.conv));
-        if (b.down) MD2_TRY(pk(b.dconv));
+        for (auto& e : b.st) pk(e.conv);
+        if (b.down) pk(b.dconv);
       }
     for (auto& d : br) {
-      MD2_TRY(pk(d.c1));
-      MD2_TRY(pk(d.c2));
-      if (d.head >= 0) MD2_TRY(pk(d.hc));
+      pk(d.c1);
+      pk(d.c2);
+      if (d.head >= 0) pk(d.hc);
     }
-    MD2_TRY(pk(sq));
-    MD2_TRY(pk(p1));
-    MD2_TRY(pk(p2));
+    pk(sq);
+    pk(p1);
+    pk(p2);
+    long blocks = 0;
+    for (auto& j : jobs) {
+      j.block_begin = blocks;
+      blocks += conv_pack_job_blocks(j);
+    }
+    void* q = nullptr;
+    MD2_HIP(hipMalloc(&q, jobs.size() * sizeof(PackJob)));
+    allocs.push_back(q);
+    MD2_HIP(hipMemcpy(q, jobs.data(), jobs.size() * sizeof(PackJob), hipMemcpyHostToDevice));
+    pack_jobs = (PackJob*)q;
+    pack_njobs = (int)jobs.size();
+    pack_blocks = blocks;
     return MD2_OK;
   }
+
+  int repack(hipStream_t st) { return conv_pack_batch(pack_jobs, pack_njobs, pack_blocks, st); }
 
   int bn_fwd(RBN& bn, const float* y, int nimg, long HW, hipStream_t st) {
     BNStatsWs w = bnws;
