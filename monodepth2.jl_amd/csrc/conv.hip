@@ -167,25 +167,51 @@ struct ConvArgs {
   const float* dy;   // dgrad / wgrad
   TensorOut out;
   float* slab;       // split-K partials [splits][M][N] or nullptr
+  // byte extents of the buffer resources (raw buffer loads: an offset past the extent reads 0,
+  // which implements the zero padding of the gathers without branches)
+  uint32_t A_bytes, b0_bytes, b1_bytes;
 };
+
+constexpr uint32_t OOB = 0x7ffffff0u;   // byte offset that is out of range for every tensor
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off_bytes, 0, 0));
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, 0);
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                     __uint_as_float(v[3]));
+}
 
 template <int TM, int TN, int BK>
 __device__ __forceinline__ void mma_chunk(const float* __restrict__ As, int lda,
                                           const float* __restrict__ Bs, int ldb, int am0, int bn0,
                                           int lane, f32x16 (&acc)[TM][TN]) {
   const int kh = lane >> 5, l = lane & 31;
+  // fragments of k-step kk+1 are read while the MFMAs of kk issue (register double buffer;
+  // fully unrolled so every index is static)
+  float a[2][TM], b[2][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) a[0][i] = As[kh * lda + am0 + i * 32 + l];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) b[0][j] = Bs[kh * ldb + bn0 + j * 32 + l];
 #pragma unroll
   for (int kk = 0; kk < BK / 2; ++kk) {
-    float a[TM], b[TN];
+    const int cur = kk & 1, nxt = cur ^ 1;
+    if (kk + 1 < BK / 2) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) a[i] = As[(2 * kk + kh) * lda + am0 + i * 32 + l];
+      for (int i = 0; i < TM; ++i) a[nxt][i] = As[(2 * kk + 2 + kh) * lda + am0 + i * 32 + l];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) b[j] = Bs[(2 * kk + kh) * ldb + bn0 + j * 32 + l];
+      for (int j = 0; j < TN; ++j) b[nxt][j] = Bs[(2 * kk + 2 + kh) * ldb + bn0 + j * 32 + l];
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][i], b[cur][j], acc[i][j], 0, 0, 0);
   }
 }
 
@@ -202,184 +228,7 @@ __device__ __forceinline__ void store_out(const TensorOut& o, int m, int img, lo
     *dst = v;
 }
 
-// ---------------------------------------------------------------------------------------------
-// forward / dgrad kernel (B operand lanes along pixels)
-// MODE 0 = forward (im2col of x), MODE 1 = dgrad (gather of dY)
-// ---------------------------------------------------------------------------------------------
-template <int MODE, int BM, int BN, int BK, int WM, int WN, int KH, int KW, int S, int RFL>
-__global__ __launch_bounds__(256) void conv_px_kernel(ConvArgs a) {
-  constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN);
-  constexpr int KK = KH * KW;
-  constexpr int A_TOT = BK * BM / 4;
-  constexpr int A_F4 = (A_TOT + 255) / 256;
-  constexpr int B_RS = 256 / BN;
-  constexpr int B_EL = BK / B_RS;
-  static_assert(A_F4 >= 1 && B_EL >= 1 && TM >= 1 && TN >= 1, "tile");
-  __shared__ __attribute__((aligned(16))) float As[2][BK][BM];
-  __shared__ float Bs[2][BK][BN];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const int m0 = blockIdx.y * BM;
-  const long n0 = (long)blockIdx.x * BN;
-  const int kbeg = blockIdx.z * a.g.kper;
-  const int kend = min(a.g.K, kbeg + a.g.kper);
-  const int nk = (kend - kbeg + BK - 1) / BK;
-
-  // ---- per-thread pixel of the B operand
-  const int bn = tid % BN;
-  const int brow = __builtin_amdgcn_readfirstlane(tid / BN);
-  const long n = n0 + bn;
-  const bool nvalid = n < a.g.N;
-  int py = 0, px = 0;
-  const float* base0 = nullptr;
-  const float* base1 = nullptr;
-  if (nvalid) {
-    const int img = (int)fdiv((uint32_t)n, a.fd_pix);
-    const int pix = (int)(n - (long)img * a.fd_pix.d);
-    const int oy = (int)fdiv((uint32_t)pix, a.fd_row);
-    const int ox = pix - oy * (int)a.fd_row.d;
-    if (MODE == 0) {
-      py = oy * S - a.pad;
-      px = ox * S - a.pad;
-      const int q = (int)fdiv((uint32_t)img, a.fd_bdiv);
-      base0 = a.in.p0 + (long)(img - q * (int)a.fd_bdiv.d) * a.in.bs0 + (long)q * a.in.bhi;
-      base1 = a.in.p1 ? a.in.p1 + (long)img * a.in.bs1 : nullptr;
-    } else {
-      py = oy;   // dX pixel (ih, iw)
-      px = ox;
-      base0 = a.dy + (long)img * a.Cout * a.HoWo;
-    }
-  }
-
-  float4 areg[A_F4];
-  float breg[B_EL];
-
-  auto load_a = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < A_F4; ++j) {
-      const int idx = tid + 256 * j;
-      const int row = idx / (BM / 4), c4 = idx % (BM / 4);
-      if (A_TOT % 256 == 0 || idx < A_TOT)
-        areg[j] = *reinterpret_cast<const float4*>(a.A + (long)(k0 + row) * a.g.Mpad + m0 + c4 * 4);
-    }
-  };
-  auto load_b = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < B_EL; ++j) {
-      const int k = k0 + brow + j * B_RS;   // wave-uniform
-      float v = 0.f;
-      if (k < kend) {
-        const int c = k / KK;
-        const int r = k - c * KK;
-        const int kh = r / KW, kw = r - (r / KW) * KW;
-        if (MODE == 0) {
-          int iy = py + kh, ix = px + kw;
-          bool ok = nvalid;
-          if (RFL) {
-            iy = refl(iy, a.H);
-            ix = refl(ix, a.W);
-          } else {
-            ok = ok && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-          }
-          const float* src = (c < a.in.c0) ? base0 + (long)c * a.HW : base1 + (long)(c - a.in.c0) * a.HW;
-          if (ok) v = src[iy * a.W + ix];
-        } else {
-          const float* d = base0 + (long)c * a.HoWo;
-          if (!RFL) {
-            const int ohn = py + a.pad - kh, own = px + a.pad - kw;
-            if (S == 1) {
-              if (nvalid && (unsigned)ohn < (unsigned)a.Ho && (unsigned)own < (unsigned)a.Wo)
-                v = d[ohn * a.Wo + own];
-            } else {
-              if (nvalid && ohn >= 0 && own >= 0 && (ohn % S) == 0 && (own % S) == 0) {
-                const int oh = ohn / S, ow = own / S;
-                if (oh < a.Ho && ow < a.Wo) v = d[oh * a.Wo + ow];
-              }
-            }
-          } else if (nvalid) {
-            // pad_reflect adjoint: padded rows q with reflect(q-1) == iy are iy+1, 0 (iy == 1)
-            // and H+1 (iy == H-2); same for columns (stride 1, pad 1).
-            const int qy[3] = {py + 1, (py == 1) ? 0 : -1000, (py == a.H - 2) ? a.H + 1 : -1000};
-            const int qx[3] = {px + 1, (px == 1) ? 0 : -1000, (px == a.W - 2) ? a.W + 1 : -1000};
-#pragma unroll
-            for (int u = 0; u < 3; ++u) {
-              const int oh = qy[u] - kh;
-              if ((unsigned)oh >= (unsigned)a.Ho) continue;
-#pragma unroll
-              for (int w = 0; w < 3; ++w) {
-                const int ow = qx[w] - kw;
-                if ((unsigned)ow >= (unsigned)a.Wo) continue;
-                v += d[oh * a.Wo + ow];
-              }
-            }
-          }
-        }
-      }
-      breg[j] = v;
-    }
-  };
-  auto store_tiles = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < A_F4; ++j) {
-      const int idx = tid + 256 * j;
-      const int row = idx / (BM / 4), c4 = idx % (BM / 4);
-      if (A_TOT % 256 == 0 || idx < A_TOT) *reinterpret_cast<float4*>(&As[buf][row][c4 * 4]) = areg[j];
-    }
-#pragma unroll
-    for (int j = 0; j < B_EL; ++j) Bs[buf][brow + j * B_RS][bn] = breg[j];
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  load_a(kbeg);
-  load_b(kbeg);
-  store_tiles(0);
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nk) {
-      load_a(kbeg + (t + 1) * BK);
-      load_b(kbeg + (t + 1) * BK);
-    }
-    mma_chunk<TM, TN, BK>(&As[cur][0][0], BM, &Bs[cur][0][0], BN, wm * TM * 32, wn * TN * 32, lane, acc);
-    if (t + 1 < nk) store_tiles(cur ^ 1);
-    __syncthreads();
-  }
-
-  // ---- epilogue
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const long nn = n0 + wn * TN * 32 + j * 32 + (lane & 31);
-    if (nn >= a.g.N) continue;
-    if (a.slab) {
-      float* sl = a.slab + (long)blockIdx.z * a.g.M * a.g.N;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (m < a.g.M) sl[(long)m * a.g.N + nn] = acc[i][j][r];
-        }
-    } else {
-      const int img = (int)fdiv((uint32_t)nn, a.fd_pix);
-      const long pix = nn - (long)img * a.fd_pix.d;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (m < a.g.M) store_out(a.out, m, img, pix, a.fd_pix.d, acc[i][j][r]);
-        }
-    }
-  }
-}
+#include "conv_px.inc"
 
 // split-K reduction + epilogue for fwd / dgrad
 __global__ __launch_bounds__(256) void splitk_reduce_px_kernel(ConvArgs a, int splits) {
@@ -628,7 +477,11 @@ Plan plan_px(int M, long N, int K) {
 
 Plan plan_w(int M, long N, long K) {
   Plan p{};
-  p.BM = 64; p.BN = 128; p.BK = 32;
+  if (M <= 32) {          // decoder 16/32-channel layers: do not pad Cout to 64
+    p.tile = 1; p.BM = 32; p.BN = 256; p.BK = 32;
+  } else {
+    p.tile = 0; p.BM = 64; p.BN = 128; p.BK = 32;
+  }
   const long tiles = (long)cdiv(M, p.BM) * cdiv(N, p.BN);
   long splits = std::max(1L, (long)512 / tiles);   // 2 blocks/CU resident (191 VGPR+AGPR)
   splits = std::min(splits, std::max(1L, K / (8 * p.BK)));
@@ -740,6 +593,17 @@ int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const 
   a.in = x;
   a.A = wpacked;
   a.out = y;
+  a.A_bytes = (uint32_t)(conv_fwd_packed_elems(s) * sizeof(float));
+  {
+    long ext0 = 0;
+    for (int b = 0; b < s.N; ++b)
+      ext0 = std::max(ext0, (long)(b % x.bdiv) * x.bs0 + (long)(b / x.bdiv) * x.bhi);
+    ext0 += (long)x.c0 * s.H * s.W;
+    const long ext1 = x.p1 ? (long)(s.N - 1) * x.bs1 + (long)(s.Cin - x.c0) * s.H * s.W : 0;
+    MD2_CHECK_ARG(ext0 * 4 < (long)OOB && ext1 * 4 < (long)OOB, "conv_fwd: tensor exceeds 2 GB");
+    a.b0_bytes = (uint32_t)(ext0 * 4);
+    a.b1_bytes = (uint32_t)(ext1 * 4);
+  }
   const Plan p = plan_px(a.g.M, a.g.N, a.g.K);
   return launch_px<0>(s, a, p, ws, st);
 }
@@ -761,6 +625,10 @@ int conv_dgrad(const ConvShape& s, const float* dy, const float* wpacked_d, cons
   a.dy = dy;
   a.A = wpacked_d;
   a.out = dx;
+  a.A_bytes = (uint32_t)(conv_dgrad_packed_elems(s) * sizeof(float));
+  MD2_CHECK_ARG((long)s.N * s.Cout * s.Ho * s.Wo * 4 < (long)OOB, "conv_dgrad: tensor exceeds 2 GB");
+  a.b0_bytes = (uint32_t)((long)s.N * s.Cout * s.Ho * s.Wo * 4);
+  a.b1_bytes = 0;
   const Plan p = plan_px(a.g.M, a.g.N, a.g.K);
   return launch_px<1>(s, a, p, ws, st);
 }
@@ -793,8 +661,12 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
   bool launched = false;
 #define MD2_W_CASE(KS, SS, RR)                                                                     \
   if (!launched && s.KH == KS && s.stride == SS && s.reflect == RR) {                              \
-    hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 32, 2, 2, KS, KS, SS, RR>), grid, dim3(256), 0, \
-                       st, a);                                                                     \
+    if (p.tile == 1)                                                                               \
+      hipLaunchKernelGGL((conv_wgrad_kernel<32, 256, 32, 1, 4, KS, KS, SS, RR>), grid, dim3(256),  \
+                         0, st, a);                                                                \
+    else                                                                                           \
+      hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 32, 2, 2, KS, KS, SS, RR>), grid, dim3(256),  \
+                         0, st, a);                                                                \
     launched = true;                                                                               \
   }
   MD2_CONV_COMBOS(MD2_W_CASE)
