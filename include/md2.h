@@ -176,6 +176,16 @@ int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const fl
 #define MD2_PROF_NCAT 3
 int md2_model_set_profiling(md2_model* m, int on);
 int md2_model_profile_read(md2_model* m, double* out, int ncat);
+/* Diagnostics (parity tests): named internal buffers of the last forward / backward, by index
+ * 0..count-1 (MD2_EINVAL past the end): encoder activations ("stem.y", "stem.out",
+ * "maxpool.out", "maxpool.arg" = window index kh*3+kw as uint8, "layer<s>.<b>.conv<k>.y",
+ * "...relu1", "....out", "....down.y"), block-output gradients "....d_out", pose activations
+ * "pose.sq", "pose.conv1", "pose.conv2", decoder skip gradients "d_skip<f>", "d_mp", "d_f0".
+ * Images are in the encoder's frame-major order (image = frame*batch + n).
+ * dims = {images, channels, height, width, dtype (0 float32, 1 uint8)}; *name valid until the
+ * next call. */
+int md2_model_debug_tensor(md2_model* m, int index, const char** name, const void** ptr,
+                           int* dims);
 /* eval_disparity (src/model.jl:63) on x [n][c][h][w], n <= batch; disp: per-level pointers */
 int md2_model_eval_disparity(md2_model* m, const float* x, int n, const float** disp,
                              void* stream);

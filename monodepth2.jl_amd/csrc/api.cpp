@@ -306,6 +306,12 @@ int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const fl
   return model_outputs(m->impl, disp, w, h, pose);
 }
 
+int md2_model_debug_tensor(md2_model* m, int index, const char** name, const void** ptr,
+                           int* dims) {
+  MD2_CHECK_ARG(m, "model");
+  return model_debug_tensor(m->impl, index, name, ptr, dims);
+}
+
 int md2_model_eval_disparity(md2_model* m, const float* x, int n, const float** disp,
                              void* stream) {
   MD2_CHECK_ARG(m, "model");

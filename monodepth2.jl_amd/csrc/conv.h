@@ -46,6 +46,13 @@ struct ConvWorkspace {
   size_t bytes = 0;
 };
 
+// GEMM reduction order.  Tap-major (k = tap*C + c, tap = kh*KW + kw) keeps the filter tap
+// constant over a K chunk, so the spatial gather address is computed once per chunk and every
+// channel step is a scalar offset; it needs the channel count (and a concat split) to be a
+// multiple of the chunk.  Otherwise (the 3-channel stem, 1-channel disparity heads) the order is
+// channel-major k = c*KK + tap.  mode: 0 forward (C = Cin), 1 dgrad (C = Cout), 2 wgrad columns.
+bool conv_tap_major(const ConvShape& s, int mode);
+
 // packed operand sizes (elements) -- weights are repacked K-major with zero padding
 size_t conv_fwd_packed_elems(const ConvShape& s);
 size_t conv_dgrad_packed_elems(const ConvShape& s);
@@ -57,6 +64,7 @@ struct PackJob {
   const float* w;
   float* out;
   int mode;            // 0 forward, 1 dgrad
+  int tap;             // tap-major K order (conv_tap_major)
   int Cout, Cin, KK, Kpad, Mpad;
   long block_begin;    // first 256-element block of this job in the batched grid
 };

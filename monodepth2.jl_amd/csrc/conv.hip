@@ -38,27 +38,28 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // ---------------------------------------------------------------------------------------------
 // weight packing
 // ---------------------------------------------------------------------------------------------
-// forward:  Wt[k][m] = W[m][k],               k = ci*KK + kh*KW + kw     ([Kpad][Mpad])
-__global__ void pack_fwd_kernel(const float* __restrict__ w, float* __restrict__ out, int M, int K,
-                                int Kpad, int Mpad) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)Kpad * Mpad) return;
-  const int k = (int)(idx / Mpad), m = (int)(idx % Mpad);
-  out[idx] = (k < K && m < M) ? w[(long)m * K + k] : 0.f;
+// forward:  Wt[k][m] = W[m][c][tap]   ([Kpad][Mpad]);   dgrad: Wd[k][ci] = W[co][ci][tap]
+// ([Kdpad][Cinpad]); k = tap*C + c (tap-major) or c*KK + tap, C = Cin (forward) / Cout (dgrad)
+__device__ __forceinline__ float pack_value(const PackJob& j, long idx) {
+  const int k = (int)(idx / j.Mpad), m = (int)(idx % j.Mpad);
+  const int C = j.mode == 0 ? j.Cin : j.Cout;     // reduction channels
+  const int Mr = j.mode == 0 ? j.Cout : j.Cin;    // rows
+  if (k >= C * j.KK || m >= Mr) return 0.f;
+  int c, tap;
+  if (j.tap) {
+    tap = k / C;
+    c = k - tap * C;
+  } else {
+    c = k / j.KK;
+    tap = k - c * j.KK;
+  }
+  const long co = j.mode == 0 ? m : c, ci = j.mode == 0 ? c : m;
+  return j.w[(co * j.Cin + ci) * j.KK + tap];
 }
 
-// dgrad:    Wd[k'][ci] = W[co][ci][kh][kw],   k' = co*KK + kh*KW + kw    ([Kdpad][Cinpad])
-__global__ void pack_dgrad_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout,
-                                  int Cin, int KK, int Kpad, int Mpad) {
+__global__ __launch_bounds__(256) void pack_one_kernel(PackJob j) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)Kpad * Mpad) return;
-  const int k = (int)(idx / Mpad), ci = (int)(idx % Mpad);
-  float v = 0.f;
-  if (k < Cout * KK && ci < Cin) {
-    const int co = k / KK, r = k % KK;
-    v = w[((long)co * Cin + ci) * KK + r];
-  }
-  out[idx] = v;
+  if (idx < (long)j.Kpad * j.Mpad) j.out[idx] = pack_value(j, idx);
 }
 
 size_t conv_fwd_packed_elems(const ConvShape& s) {
@@ -68,31 +69,12 @@ size_t conv_dgrad_packed_elems(const ConvShape& s) {
   return (size_t)round_up((long)s.Cout * s.KH * s.KW, KPAD) * round_up(s.Cin, MPAD);
 }
 
-int conv_pack_fwd(const ConvShape& s, const float* w, float* packed, hipStream_t st) {
-  const int K = s.Cin * s.KH * s.KW;
-  const int Kpad = (int)round_up(K, KPAD), Mpad = (int)round_up(s.Cout, MPAD);
-  const long total = (long)Kpad * Mpad;
-  hipLaunchKernelGGL(pack_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, w, packed, s.Cout,
-                     K, Kpad, Mpad);
-  MD2_LAUNCH_CHECK();
-  return MD2_OK;
-}
-
-int conv_pack_dgrad(const ConvShape& s, const float* w, float* packed, hipStream_t st) {
-  const int KK = s.KH * s.KW;
-  const int Kpad = (int)round_up((long)s.Cout * KK, KPAD), Mpad = (int)round_up(s.Cin, MPAD);
-  const long total = (long)Kpad * Mpad;
-  hipLaunchKernelGGL(pack_dgrad_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, w, packed,
-                     s.Cout, s.Cin, KK, Kpad, Mpad);
-  MD2_LAUNCH_CHECK();
-  return MD2_OK;
-}
-
 PackJob conv_pack_job(const ConvShape& s, int mode, const float* w, float* out) {
   PackJob j{};
   j.w = w;
   j.out = out;
   j.mode = mode;
+  j.tap = conv_tap_major(s, mode) ? 1 : 0;
   j.Cout = s.Cout;
   j.Cin = s.Cin;
   j.KK = s.KH * s.KW;
@@ -108,6 +90,19 @@ PackJob conv_pack_job(const ConvShape& s, int mode, const float* w, float* out) 
 
 long conv_pack_job_blocks(const PackJob& j) { return cdiv((long)j.Kpad * j.Mpad, 256); }
 
+static int pack_single(const ConvShape& s, int mode, const float* w, float* packed, hipStream_t st) {
+  const PackJob j = conv_pack_job(s, mode, w, packed);
+  hipLaunchKernelGGL(pack_one_kernel, dim3(conv_pack_job_blocks(j)), dim3(256), 0, st, j);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+int conv_pack_fwd(const ConvShape& s, const float* w, float* packed, hipStream_t st) {
+  return pack_single(s, 0, w, packed, st);
+}
+int conv_pack_dgrad(const ConvShape& s, const float* w, float* packed, hipStream_t st) {
+  return pack_single(s, 1, w, packed, st);
+}
+
 __global__ __launch_bounds__(256) void pack_batch_kernel(const PackJob* __restrict__ jobs, int njobs) {
   // find the job of this block (jobs sorted by block_begin; few dozen entries)
   __shared__ int s_job;
@@ -122,19 +117,7 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const PackJob* __restri
   __syncthreads();
   const PackJob j = jobs[s_job];
   const long idx = ((long)blockIdx.x - j.block_begin) * 256 + threadIdx.x;
-  if (idx >= (long)j.Kpad * j.Mpad) return;
-  const int k = (int)(idx / j.Mpad), m = (int)(idx % j.Mpad);
-  float v = 0.f;
-  if (j.mode == 0) {
-    const int K = j.Cin * j.KK;
-    if (k < K && m < j.Cout) v = j.w[(long)m * K + k];
-  } else {
-    if (k < j.Cout * j.KK && m < j.Cin) {
-      const int co = k / j.KK, r = k % j.KK;
-      v = j.w[((long)co * j.Cin + m) * j.KK + r];
-    }
-  }
-  j.out[idx] = v;
+  if (idx < (long)j.Kpad * j.Mpad) j.out[idx] = pack_value(j, idx);
 }
 
 int conv_pack_batch(const PackJob* dev_jobs, int njobs, long total_blocks, hipStream_t st) {
@@ -170,6 +153,7 @@ struct ConvArgs {
   // byte extents of the buffer resources (raw buffer loads: an offset past the extent reads 0,
   // which implements the zero padding of the gathers without branches)
   uint32_t A_bytes, b0_bytes, b1_bytes;
+  uint32_t HW4, HoWo4;   // channel strides in bytes (scalar soffset steps of the tap-major gathers)
 };
 
 constexpr uint32_t OOB = 0x7ffffff0u;   // byte offset that is out of range for every tensor
@@ -179,6 +163,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint3
 }
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off_bytes, 0, 0));
+}
+// voffset (per lane; OOB for padding) + soffset (wave-uniform channel step); OOB + soffset stays
+// below 2^32 and beyond every extent, whether or not the range check includes soffset
+__device__ __forceinline__ float bload_s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
 }
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, 0);
@@ -357,6 +346,130 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   }
 }
 
+// tap-major wgrad: filter columns n = tap*Cin + c.  A block covers TT = BN/CW consecutive taps
+// x CW channels (CW | Cin, and CW | the concat split, so the block reads one tensor): row j of a
+// thread is tap (RP*j)/CW and channel (RP*j)%CW + rg, both compile-time up to the block base.
+// Per K chunk each thread computes one gather offset per tap (TT of them); every element is then
+// a buffer load with that offset and a scalar channel soffset -- no VALU per element.  The slab
+// is written in (m, n) tap-major order; the final reduction permutes to [Cout][Cin][KH][KW].
+template <int BM, int BN, int BK, int WM, int WN, int KH, int KW, int S, int RFL, int CW>
+__global__ __launch_bounds__(256) void conv_wgrad_tap_kernel(ConvArgs a) {
+  constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN);
+  constexpr int KK = KH * KW;
+  constexpr int RP = 256 / BK;          // rows per pass
+  constexpr int A_EL = BM / RP, B_EL = BN / RP;
+  constexpr int TT = BN / CW;           // taps per block
+  constexpr int LDA = BM + 1, LDB = BN + 1;
+  static_assert(A_EL >= 1 && B_EL >= 1 && TT >= 1 && CW % RP == 0, "tile");
+  __shared__ float As[2][BK][LDA];
+  __shared__ float Bs[2][BK][LDB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int m0 = blockIdx.y * BM;
+  const int ncb = a.Cin / CW;
+  const int tb = (int)blockIdx.x / ncb * TT;           // first tap of the block
+  const int cbk = ((int)blockIdx.x % ncb) * CW;        // first channel of the block
+  const int kbeg = blockIdx.z * a.g.kper;
+  const int kend = min(a.g.K, kbeg + a.g.kper);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int kl = tid % BK;
+  const int rg = tid / BK;
+  const int mlim = a.g.M - m0 - rg;     // row j of dY valid iff RP*j < mlim
+
+  const bool sec = cbk >= a.in.c0;      // block-uniform concat side
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(a.dy, a.A_bytes);
+  const __amdgpu_buffer_rsrc_t rx = sec ? make_rsrc(a.in.p1, a.b1_bytes) : make_rsrc(a.in.p0, a.b0_bytes);
+  const uint32_t cso = (uint32_t)(sec ? cbk - a.in.c0 : cbk) * a.HW4;
+
+  float areg[A_EL], breg[B_EL];
+
+  // all offsets in 32 bits: every extent is < 2 GB (checked on the host)
+#define MD2_W_LOAD(K0)                                                                            \
+  {                                                                                               \
+    const int p = (K0) + kl;                                                                      \
+    const bool pv = p < kend;                                                                     \
+    const uint32_t pc = (uint32_t)(pv ? p : kbeg);                                                \
+    const uint32_t img = fdiv(pc, a.fd_pix);                                                      \
+    const uint32_t pix = pc - img * a.fd_pix.d;                                                   \
+    const uint32_t oy = fdiv(pix, a.fd_row);                                                      \
+    const uint32_t ox = pix - oy * a.fd_row.d;                                                    \
+    const uint32_t va = pv ? ((img * (uint32_t)a.Cout + rg) * (uint32_t)a.HoWo + pix) * 4u : OOB; \
+    _Pragma("unroll") for (int j = 0; j < A_EL; ++j)                                              \
+      areg[j] = bload_s(rdy, RP * j < mlim ? va : OOB, (uint32_t)(m0 + RP * j) * a.HoWo4);        \
+    uint32_t vb;                                                                                  \
+    if (sec) {                                                                                    \
+      vb = (img * (uint32_t)a.in.bs1 + rg * (uint32_t)a.HW) * 4u;                                 \
+    } else {                                                                                      \
+      const uint32_t q = fdiv(img, a.fd_bdiv);                                                    \
+      vb = ((img - q * a.fd_bdiv.d) * (uint32_t)a.in.bs0 + q * (uint32_t)a.in.bhi +               \
+            rg * (uint32_t)a.HW) * 4u;                                                            \
+    }                                                                                             \
+    const int py = (int)oy * S - a.pad, px = (int)ox * S - a.pad;                                 \
+    uint32_t vt[TT];                                                                              \
+    _Pragma("unroll") for (int t = 0; t < TT; ++t) {                                              \
+      const int tap = tb + t;                                                                     \
+      const int kh = tap / KW, kw = tap - (tap / KW) * KW;                                        \
+      int iy = py + kh, ix = px + kw;                                                             \
+      bool ok;                                                                                    \
+      if (RFL) {                                                                                  \
+        iy = refl(iy, a.H);                                                                       \
+        ix = refl(ix, a.W);                                                                       \
+        ok = pv;                                                                                  \
+      } else {                                                                                    \
+        ok = pv && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;                  \
+      }                                                                                           \
+      vt[t] = (ok && tap < KK) ? vb + (uint32_t)(iy * a.W + ix) * 4u : OOB;                       \
+    }                                                                                             \
+    _Pragma("unroll") for (int j = 0; j < B_EL; ++j)                                              \
+      breg[j] = bload_s(rx, vt[(RP * j) / CW], cso + (uint32_t)((RP * j) % CW) * a.HW4);         \
+  }
+#define MD2_W_STORE(BUF)                                                                          \
+  _Pragma("unroll") for (int j = 0; j < A_EL; ++j) As[BUF][kl][rg + j * RP] = areg[j];            \
+  _Pragma("unroll") for (int j = 0; j < B_EL; ++j) Bs[BUF][kl][rg + j * RP] = breg[j];
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) {
+    MD2_W_LOAD(kbeg);
+    MD2_W_STORE(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) MD2_W_LOAD(kbeg + (t + 1) * BK);
+    mma_chunk<TM, TN, BK>(&As[cur][0][0], LDA, &Bs[cur][0][0], LDB, wm * TM * 32, wn * TN * 32, lane, acc);
+    if (t + 1 < nk) {
+      MD2_W_STORE(cur ^ 1);
+    }
+    __syncthreads();
+  }
+#undef MD2_W_LOAD
+#undef MD2_W_STORE
+
+  float* sl = a.slab + (long)blockIdx.z * a.g.M * a.g.N;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = wn * TN * 32 + j * 32 + (lane & 31);
+    const int tap = tb + nl / CW;
+    if (tap >= KK) continue;
+    const long nn = (long)tap * a.Cin + cbk + nl % CW;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < a.g.M) sl[(long)m * a.g.N + nn] = acc[i][j][r];
+      }
+  }
+}
+
 // split-K slab reduction for wgrad, two stages for parallelism: stage 1 sums split groups
 // (group g takes splits g, g+G, ...) into part[G][total]; stage 2 sums the G partials.
 constexpr int WRED_GROUPS = 32;
@@ -377,17 +490,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_w1_kernel(const float* __re
   part[(long)g * total + idx] = v0 + v1;
 }
 
+// stage 2; tapc > 0: slab columns are tap-major (n = tap*Cin + c, Cin = tapc) and are written
+// to the [Cout][Cin][KK] parameter layout
 __global__ __launch_bounds__(256) void splitk_reduce_w2_kernel(const float* __restrict__ part,
                                                                int G, long total,
-                                                               float* __restrict__ dw, int acc) {
+                                                               float* __restrict__ dw, int acc,
+                                                               int ncols, int tapc, int KK) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
   float v = 0.f;
   for (int g = 0; g < G; ++g) v += part[(long)g * total + idx];
+  long o = idx;
+  if (tapc > 0) {
+    const long m = idx / ncols;
+    const int n = (int)(idx - m * ncols);
+    const int tp = n / tapc, c = n - tp * tapc;
+    o = m * ncols + (long)c * KK + tp;
+  }
   if (acc)
-    dw[idx] += v;
+    dw[o] += v;
   else
-    dw[idx] = v;
+    dw[o] = v;
 }
 
 // bias gradient db[c] = sum over images and pixels of dY[img][c][:], two stages:
@@ -475,19 +598,48 @@ Plan plan_px(int M, long N, int K) {
   return p;
 }
 
-Plan plan_w(int M, long N, long K) {
+// wgrad: n_tiles = column tiles (tap-major: tap groups x channel blocks)
+Plan plan_w(int M, long n_tiles_128, long n_tiles_256, long K) {
   Plan p{};
   if (M <= 32) {          // decoder 16/32-channel layers: do not pad Cout to 64
     p.tile = 1; p.BM = 32; p.BN = 256; p.BK = 32;
   } else {
     p.tile = 0; p.BM = 64; p.BN = 128; p.BK = 32;
   }
-  const long tiles = (long)cdiv(M, p.BM) * cdiv(N, p.BN);
-  long splits = std::max(1L, (long)512 / tiles);   // 2 blocks/CU resident (191 VGPR+AGPR)
+  const long tiles = (long)cdiv(M, p.BM) * (p.tile == 1 ? n_tiles_256 : n_tiles_128);
+  long splits = std::max(1L, (long)512 / tiles);   // 2 blocks/CU resident
   splits = std::min(splits, std::max(1L, K / (8 * p.BK)));
   p.kper = (int)round_up((K + splits - 1) / splits, p.BK);
   p.splits = (int)((K + p.kper - 1) / p.kper);
   return p;
+}
+
+// channels per tap block of the tap-major wgrad: largest of 128/64/32/16 dividing Cin and the
+// concat split
+int wgrad_cw(const ConvShape& s, int c0) {
+  for (int cw = 128; cw >= 16; cw /= 2)
+    if (s.Cin % cw == 0 && (c0 >= s.Cin || c0 % cw == 0)) return cw;
+  return 0;
+}
+
+struct WTiles {
+  int cw;          // 0: channel-major kernel
+  long n128, n256; // column tiles for BN = 128 / 256
+};
+
+WTiles wgrad_tiles(const ConvShape& s, int c0) {
+  WTiles t{};
+  const int KK = s.KH * s.KW;
+  const long N = (long)s.Cin * KK;
+  t.cw = conv_tap_major(s, 2) ? wgrad_cw(s, c0) : 0;
+  if (t.cw) {
+    t.n128 = (long)cdiv(KK, std::max(1, 128 / t.cw)) * (s.Cin / t.cw);
+    t.n256 = (long)cdiv(KK, 256 / t.cw) * (s.Cin / t.cw);
+  } else {
+    t.n128 = cdiv(N, 128);
+    t.n256 = cdiv(N, 256);
+  }
+  return t;
 }
 
 void fill_common(ConvArgs& a, const ConvShape& s) {
@@ -495,6 +647,8 @@ void fill_common(ConvArgs& a, const ConvShape& s) {
   a.stride = s.stride; a.pad = s.pad;
   a.HW = (long)s.H * s.W;
   a.HoWo = (long)s.Ho * s.Wo;
+  a.HW4 = (uint32_t)(a.HW * 4);
+  a.HoWo4 = (uint32_t)(a.HoWo * 4);
 }
 
 int check_shape(const ConvShape& s) {
@@ -514,11 +668,15 @@ int check_shape(const ConvShape& s) {
 #define MD2_CONV_COMBOS(X) X(1, 1, 0) X(1, 2, 0) X(3, 1, 0) X(3, 1, 1) X(3, 2, 0) X(7, 2, 0)
 
 template <int MODE, int BM, int BN, int WM, int WN>
-int launch_px_tile(const ConvShape& s, const ConvArgs& a, dim3 grid, hipStream_t st) {
+int launch_px_tile(const ConvShape& s, const ConvArgs& a, bool tap, dim3 grid, hipStream_t st) {
 #define MD2_PX_CASE(KS, SS, RR)                                                                  \
   if (s.KH == KS && s.stride == SS && s.reflect == RR) {                                         \
-    hipLaunchKernelGGL((conv_px_kernel<MODE, BM, BN, 16, WM, WN, KS, KS, SS, RR>), grid, dim3(256), \
-                       0, st, a);                                                                \
+    if (tap)                                                                                     \
+      hipLaunchKernelGGL((conv_px_kernel<MODE, 1, BM, BN, 16, WM, WN, KS, KS, SS, RR>), grid,    \
+                         dim3(256), 0, st, a);                                                   \
+    else                                                                                         \
+      hipLaunchKernelGGL((conv_px_kernel<MODE, 0, BM, BN, 16, WM, WN, KS, KS, SS, RR>), grid,    \
+                         dim3(256), 0, st, a);                                                   \
     MD2_LAUNCH_CHECK();                                                                          \
     return MD2_OK;                                                                               \
   }
@@ -538,11 +696,12 @@ int launch_px(const ConvShape& s, ConvArgs& a, const Plan& p, ConvWorkspace ws, 
     a.slab = (float*)ws.ptr;
   }
   dim3 grid(cdiv(a.g.N, p.BN), cdiv(a.g.M, p.BM), p.splits);
+  const bool tap = conv_tap_major(s, MODE);
   int rc;
   switch (p.tile) {
-    case T128x128: rc = launch_px_tile<MODE, 128, 128, 2, 2>(s, a, grid, st); break;
-    case T64x256: rc = launch_px_tile<MODE, 64, 256, 1, 4>(s, a, grid, st); break;
-    default: rc = launch_px_tile<MODE, 32, 256, 1, 4>(s, a, grid, st); break;
+    case T128x128: rc = launch_px_tile<MODE, 128, 128, 2, 2>(s, a, tap, grid, st); break;
+    case T64x256: rc = launch_px_tile<MODE, 64, 256, 1, 4>(s, a, tap, grid, st); break;
+    default: rc = launch_px_tile<MODE, 32, 256, 1, 4>(s, a, tap, grid, st); break;
   }
   if (rc) return rc;
   if (p.splits > 1) {
@@ -553,7 +712,41 @@ int launch_px(const ConvShape& s, ConvArgs& a, const Plan& p, ConvWorkspace ws, 
   return MD2_OK;
 }
 
+template <int BM, int BN, int WM, int WN, int KS, int SS, int RR>
+int launch_w(int cw, const ConvArgs& a, dim3 grid, hipStream_t st) {
+  switch (cw) {
+    case 0:
+      hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, 32, WM, WN, KS, KS, SS, RR>), grid, dim3(256), 0,
+                         st, a);
+      break;
+#define MD2_W_CW(CW)                                                                               \
+  case CW:                                                                                         \
+    hipLaunchKernelGGL((conv_wgrad_tap_kernel<BM, BN, 32, WM, WN, KS, KS, SS, RR, CW>), grid,       \
+                       dim3(256), 0, st, a);                                                       \
+    break;
+      MD2_W_CW(16) MD2_W_CW(32) MD2_W_CW(64) MD2_W_CW(128)
+#undef MD2_W_CW
+    default: return MD2_ENOTSUP;
+  }
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 }  // namespace
+
+bool conv_tap_major(const ConvShape& s, int mode) {
+  // MD2_CONV_CHANNEL_MAJOR=<bitmask of modes> forces the channel-major order (debugging)
+  static const int forced = [] {
+    const char* e = getenv("MD2_CONV_CHANNEL_MAJOR");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced & (1 << mode)) return false;
+  switch (mode) {
+    case 0: return s.Cin % 16 == 0;                                   // px chunk BK = 16
+    case 1: return s.Cout % 16 == 0 && (!s.reflect || (s.H != 3 && s.W != 3));
+    default: return s.Cin % 16 == 0;                                  // wgrad CW >= 16
+  }
+}
 
 size_t conv_fwd_workspace(const ConvShape& s) {
   const long N = (long)s.N * s.Ho * s.Wo;
@@ -567,13 +760,21 @@ size_t conv_dgrad_workspace(const ConvShape& s) {
   return p.splits > 1 ? (size_t)p.splits * s.Cin * N * sizeof(float) : 0;
 }
 
-size_t conv_wgrad_workspace(const ConvShape& s) {
+static size_t wgrad_ws_bytes(const ConvShape& s, int c0) {
   const long K = (long)s.N * s.Ho * s.Wo;
   const long Nc = (long)s.Cin * s.KH * s.KW;
-  const Plan p = plan_w(s.Cout, Nc, K);
+  const WTiles t = wgrad_tiles(s, c0);
+  const Plan p = plan_w(s.Cout, t.n128, t.n256, K);
   const size_t groups = (size_t)std::min(p.splits, WRED_GROUPS);
   return ((size_t)p.splits + groups) * s.Cout * Nc * sizeof(float) +
          (size_t)s.Cout * bias_parts(s.Cout, K) * sizeof(float) + 256;
+}
+
+// the split count depends on the concat split only through CW: size for every possible CW
+size_t conv_wgrad_workspace(const ConvShape& s) {
+  size_t b = wgrad_ws_bytes(s, s.Cin);
+  for (int c0 = 16; c0 <= 128; c0 *= 2) b = std::max(b, wgrad_ws_bytes(s, c0));
+  return b;
 }
 
 int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const TensorOut& y,
@@ -581,6 +782,8 @@ int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const 
   MD2_TRY(check_shape(s));
   MD2_CHECK_ARG(x.p0 && wpacked && y.p0, "conv_fwd pointers");
   MD2_CHECK_ARG(x.c0 == s.Cin || x.p1 != nullptr, "conv_fwd: second input tensor missing");
+  MD2_CHECK_ARG(x.c0 >= s.Cin || !conv_tap_major(s, 0) || x.c0 % 16 == 0,
+                "conv_fwd: concat split must be a multiple of 16 channels");
   ConvArgs a{};
   fill_common(a, s);
   a.g.M = s.Cout;
@@ -637,6 +840,9 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
                int accumulate, ConvWorkspace ws, hipStream_t st) {
   MD2_TRY(check_shape(s));
   MD2_CHECK_ARG(x.p0 && dy && dw, "conv_wgrad pointers");
+  MD2_CHECK_ARG(x.c0 >= s.Cin || x.p1 != nullptr, "conv_wgrad: second input tensor missing");
+  const WTiles wt = wgrad_tiles(s, x.c0);
+  const bool tap = wt.cw > 0;
   ConvArgs a{};
   fill_common(a, s);
   const long Kpix = (long)s.N * s.Ho * s.Wo;
@@ -648,7 +854,20 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
   a.fd_bdiv = make_fastdiv((uint32_t)std::min(x.bdiv, 1 << 30));
   a.in = x;
   a.dy = dy;
-  const Plan p = plan_w(a.g.M, a.g.N, Kpix);
+  {
+    long ext0 = 0;
+    for (int b = 0; b < s.N; ++b)
+      ext0 = std::max(ext0, (long)(b % x.bdiv) * x.bs0 + (long)(b / x.bdiv) * x.bhi);
+    ext0 += (long)std::min(x.c0, s.Cin) * s.H * s.W;
+    const long ext1 = x.p1 ? (long)(s.N - 1) * x.bs1 + (long)(s.Cin - x.c0) * s.H * s.W : 0;
+    const long extd = (long)s.N * s.Cout * s.Ho * s.Wo;
+    MD2_CHECK_ARG(ext0 * 4 < (long)OOB && ext1 * 4 < (long)OOB && extd * 4 < (long)OOB,
+                  "conv_wgrad: tensor exceeds 2 GB");
+    a.b0_bytes = (uint32_t)(ext0 * 4);
+    a.b1_bytes = (uint32_t)(ext1 * 4);
+    a.A_bytes = (uint32_t)(extd * 4);
+  }
+  const Plan p = plan_w(a.g.M, wt.n128, wt.n256, Kpix);
   a.g.kper = p.kper;
   const size_t need = conv_wgrad_workspace(s);
   MD2_CHECK_ARG(ws.ptr && ws.bytes >= need, "conv_wgrad workspace too small");
@@ -657,23 +876,20 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
   const int groups = std::min(p.splits, WRED_GROUPS);
   float* part = a.slab + (long)p.splits * total;
   float* bpart = part + (long)groups * total;
-  dim3 grid(cdiv(a.g.N, p.BN), cdiv(a.g.M, p.BM), p.splits);
-  bool launched = false;
+  dim3 grid((unsigned)(p.tile == 1 ? wt.n256 : wt.n128), cdiv(a.g.M, p.BM), p.splits);
+  int rc = MD2_ENOTSUP;
 #define MD2_W_CASE(KS, SS, RR)                                                                     \
-  if (!launched && s.KH == KS && s.stride == SS && s.reflect == RR) {                              \
+  if (rc == MD2_ENOTSUP && s.KH == KS && s.stride == SS && s.reflect == RR) {                      \
     if (p.tile == 1)                                                                               \
-      hipLaunchKernelGGL((conv_wgrad_kernel<32, 256, 32, 1, 4, KS, KS, SS, RR>), grid, dim3(256),  \
-                         0, st, a);                                                                \
+      rc = launch_w<32, 256, 1, 4, KS, SS, RR>(wt.cw, a, grid, st);                                \
     else                                                                                           \
-      hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 32, 2, 2, KS, KS, SS, RR>), grid, dim3(256),  \
-                         0, st, a);                                                                \
-    launched = true;                                                                               \
+      rc = launch_w<64, 128, 2, 2, KS, SS, RR>(wt.cw, a, grid, st);                                \
   }
   MD2_CONV_COMBOS(MD2_W_CASE)
 #undef MD2_W_CASE
-  if (!launched) {
+  if (rc) {
     set_error("conv_wgrad: unsupported (kernel, stride, padding) combination");
-    return MD2_ENOTSUP;
+    return rc;
   }
   MD2_LAUNCH_CHECK();
   if (groups > 1) {
@@ -681,10 +897,10 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
                        a.slab, p.splits, total, groups, part);
     MD2_LAUNCH_CHECK();
     hipLaunchKernelGGL(splitk_reduce_w2_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, part,
-                       groups, total, dw, accumulate);
+                       groups, total, dw, accumulate, (int)a.g.N, tap ? s.Cin : 0, s.KH * s.KW);
   } else {
     hipLaunchKernelGGL(splitk_reduce_w2_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a.slab,
-                       1, total, dw, accumulate);
+                       1, total, dw, accumulate, (int)a.g.N, tap ? s.Cin : 0, s.KH * s.KW);
   }
   MD2_LAUNCH_CHECK();
   if (db) {

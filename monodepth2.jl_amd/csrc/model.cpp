@@ -897,6 +897,7 @@ class Model {
   }
 
   const float* cur_x = nullptr;
+  std::string dbg_name;   // storage behind model_debug_tensor's name
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -969,6 +970,59 @@ int model_adam(Model* m, float* adam_m, float* adam_v, float lr, float b1, float
 int model_repack(Model* m, hipStream_t st) {
   MD2_CHECK_ARG(m, "model");
   return m->repack(st);
+}
+
+int model_debug_tensor(Model* m, int index, const char** name, const void** ptr, int* dims) {
+  MD2_CHECK_ARG(m && ptr && dims, "debug_tensor arguments");
+  struct T {
+    std::string name;
+    const void* p;
+    int n, c, h, w, u8;
+  };
+  const int B = m->B, N = m->N;
+  std::vector<T> ts;
+  ts.push_back({"stem.y", m->y0, B, 64, m->H0, m->W0, 0});
+  ts.push_back({"stem.out", m->f0, B, 64, m->H0, m->W0, 0});
+  ts.push_back({"maxpool.out", m->mp, B, 64, m->Hm, m->Wm, 0});
+  ts.push_back({"maxpool.arg", m->mp_arg, B, 64, m->Hm, m->Wm, 1});
+  for (size_t si = 0; si < m->stages.size(); ++si)
+    for (size_t bi = 0; bi < m->stages[si].size(); ++bi) {
+      auto& b = m->stages[si][bi];
+      const std::string pre = "layer" + std::to_string(si + 1) + "." + std::to_string(bi);
+      for (size_t k = 0; k < b.st.size(); ++k) {
+        auto& e = b.st[k];
+        const bool last = k + 1 == b.st.size();
+        ts.push_back({pre + ".conv" + std::to_string(k + 1) + ".y", e.y, B, e.conv.p.cout,
+                      e.conv.s.Ho, e.conv.s.Wo, 0});
+        ts.push_back({pre + (last ? std::string(".out") : ".relu" + std::to_string(k + 1)), e.a, B,
+                      e.conv.p.cout, e.conv.s.Ho, e.conv.s.Wo, 0});
+      }
+      if (b.down) ts.push_back({pre + ".down.y", b.yd, B, b.C, b.H, b.W, 0});
+      ts.push_back({pre + ".d_out", b.d_out, B, b.C, b.H, b.W, 0});
+    }
+  const int h4 = m->featH[4], w4 = m->featW[4];
+  ts.push_back({"pose.sq", m->sqo, B, 256, h4, w4, 0});
+  ts.push_back({"pose.conv1", m->pc1, 2 * N, 256, h4, w4, 0});
+  ts.push_back({"pose.conv2", m->pc2, 2 * N, 256, h4, w4, 0});
+  for (int f = 0; f < 4; ++f)
+    if (m->d_skip[f])
+      ts.push_back({"d_skip" + std::to_string(f), m->d_skip[f], N, m->featC[f], m->featH[f],
+                    m->featW[f], 0});
+  ts.push_back({"d_mp", m->d_mp, B, 64, m->Hm, m->Wm, 0});
+  ts.push_back({"d_f0", m->d_f0, B, 64, m->H0, m->W0, 0});
+  if (index < 0 || index >= (int)ts.size()) {
+    set_error("debug_tensor: index out of range");
+    return MD2_EINVAL;
+  }
+  m->dbg_name = ts[index].name;
+  if (name) *name = m->dbg_name.c_str();
+  *ptr = ts[index].p;
+  dims[0] = ts[index].n;
+  dims[1] = ts[index].c;
+  dims[2] = ts[index].h;
+  dims[3] = ts[index].w;
+  dims[4] = ts[index].u8;
+  return MD2_OK;
 }
 
 int model_outputs(Model* m, const float** disp, int* dw, int* dh, const float** pose) {

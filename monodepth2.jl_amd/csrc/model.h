@@ -63,6 +63,7 @@ int model_repack(Model* m, hipStream_t st);   // after the parameters changed
 int model_outputs(Model* m, const float** disp, int* dw, int* dh, const float** pose);
 // inference: eval_disparity (src/model.jl:63) on x [n][C][H][W], n <= N*3
 int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipStream_t st);
+int model_debug_tensor(Model* m, int index, const char** name, const void** ptr, int* dims);
 long model_param_count(Model* m);
 size_t model_device_bytes(Model* m);
 

@@ -202,13 +202,31 @@ class _Executor:
         pose = _wrap(pp.value, (2 * self.batch, 6), self.model.device)
         return disps, pose
 
+    def debug_tensors(self):
+        """{name: copy} of the library's internal buffers of the last forward/backward (see
+        md2_model_debug_tensor; parity diagnostics).  Images in frame-major encoder order."""
+        import torch
+        out = {}
+        dims = (C.c_int * 5)()
+        p = C.c_void_p()
+        nm = C.c_char_p()
+        i = 0
+        while lib().md2_model_debug_tensor(self.handle, i, C.byref(nm), C.byref(p), dims) == 0:
+            shape = tuple(dims[:4])
+            out[nm.value.decode()] = _wrap(p.value, shape, self.model.device,
+                                           torch.uint8 if dims[4] else torch.float32)
+            i += 1
+        return out
 
-def _wrap(p, shape, device):
+
+def _wrap(p, shape, device, dtype=None):
     """Copy library-owned device memory into a fresh torch tensor (md2_memcpy_d2d)."""
     import torch
+    dtype = dtype or torch.float32
     n = int(np.prod(shape))
-    out = torch.empty(shape, dtype=torch.float32, device=device)
-    check(lib().md2_memcpy_d2d(ptr(out), C.c_void_p(p), n * 4, stream_of(device)), "md2_memcpy_d2d")
+    out = torch.empty(shape, dtype=dtype, device=device)
+    check(lib().md2_memcpy_d2d(ptr(out), C.c_void_p(p), n * out.element_size(), stream_of(device)),
+          "md2_memcpy_d2d")
     return out
 
 

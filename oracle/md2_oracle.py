@@ -398,6 +398,50 @@ def unflatten(flat: torch.Tensor, spec):
     return out
 
 
+# Test hook: branch decisions of the forward imposed from another evaluation (the GPU run), so
+# gradients are compared on the same piecewise-smooth branch.  A ReLU whose input sits within
+# fp32 rounding of 0, or a max-pool window with a near-tie, flips its derivative under a 1e-7
+# perturbation; one flipped element among 10^4 moves every gradient below it by ~1%.  Keys:
+# "stem", "<block>.relu1", "<block>.out" (masks, 1 where the imposed output is > 0), "maxpool"
+# (window index kh*3+kw per output, padded window), "pose<j>.{sqa,sqb,conv1,conv2}".  Values
+# are unchanged up to the rounding-level input of a flipped element.
+_FORCED = None
+
+
+class forced_decisions:
+    """``with forced_decisions(d): ...`` imposes the masks / indices of dict ``d``."""
+
+    def __init__(self, d):
+        self.d = d
+
+    def __enter__(self):
+        global _FORCED
+        self.prev, _FORCED = _FORCED, self.d
+        return self
+
+    def __exit__(self, *a):
+        global _FORCED
+        _FORCED = self.prev
+
+
+def _relu(z, key):
+    if _FORCED is not None and key in _FORCED:
+        return z * _FORCED[key].to(z.dtype)
+    return F.relu(z)
+
+
+def _maxpool3x3s2(y):
+    if _FORCED is not None and "maxpool" in _FORCED:
+        idx = _FORCED["maxpool"].long()                               # [B,C,Ho,Wo]
+        B, C, H, W = y.shape
+        Ho, Wo = idx.shape[2], idx.shape[3]
+        yp = F.pad(y, (1, 1, 1, 1), value=float("-inf"))
+        win = F.unfold(yp.reshape(B * C, 1, H + 2, W + 2), 3, stride=2)  # [B*C, 9, Ho*Wo]
+        out = torch.gather(win, 1, idx.reshape(B * C, 1, Ho * Wo))
+        return out.reshape(B, C, Ho, Wo)
+    return F.max_pool2d(y, 3, stride=2, padding=1)
+
+
 def batchnorm_train(x, gamma, beta, eps=1e-5):
     """Flux ``BatchNorm`` in train mode (``trainmode!``, scripts/script.jl:86)."""
     return F.batch_norm(x, None, None, gamma, beta, training=True, momentum=0.1, eps=eps)
@@ -406,9 +450,9 @@ def batchnorm_train(x, gamma, beta, eps=1e-5):
 def resnet_stages(P, x, arch=18):
     """ResNet.jl ``encoder(x, Val(:stages))`` (src/model.jl:37) -> 5 stage features."""
     y = F.conv2d(x, P["encoder.stem.conv.weight"], stride=2, padding=3)
-    y = F.relu(batchnorm_train(y, P["encoder.stem.bn.gamma"], P["encoder.stem.bn.beta"]))
+    y = _relu(batchnorm_train(y, P["encoder.stem.bn.gamma"], P["encoder.stem.bn.beta"]), "stem")
     feats = [y]
-    y = F.max_pool2d(y, 3, stride=2, padding=1)
+    y = _maxpool3x3s2(y)
     layers = RESNET_LAYERS[arch]
     bottleneck = arch >= 50
     for si, nblocks in enumerate(layers):
@@ -420,13 +464,13 @@ def resnet_stages(P, x, arch=18):
                 h = F.relu(batchnorm_train(F.conv2d(h, P[p + ".conv2.weight"], stride=stride, padding=1), P[p + ".bn2.gamma"], P[p + ".bn2.beta"]))
                 h = batchnorm_train(F.conv2d(h, P[p + ".conv3.weight"]), P[p + ".bn3.gamma"], P[p + ".bn3.beta"])
             else:
-                h = F.relu(batchnorm_train(F.conv2d(y, P[p + ".conv1.weight"], stride=stride, padding=1), P[p + ".bn1.gamma"], P[p + ".bn1.beta"]))
+                h = _relu(batchnorm_train(F.conv2d(y, P[p + ".conv1.weight"], stride=stride, padding=1), P[p + ".bn1.gamma"], P[p + ".bn1.beta"]), p + ".relu1")
                 h = batchnorm_train(F.conv2d(h, P[p + ".conv2.weight"], padding=1), P[p + ".bn2.gamma"], P[p + ".bn2.beta"])
             if (p + ".down.weight") in P:
                 idn = batchnorm_train(F.conv2d(y, P[p + ".down.weight"], stride=stride), P[p + ".down_bn.gamma"], P[p + ".down_bn.beta"])
             else:
                 idn = y
-            y = F.relu(h + idn)
+            y = _relu(h + idn, p + ".out")
         feats.append(y)
     return feats
 
@@ -453,12 +497,12 @@ def depth_decoder(P, features, scale_levels=(2, 3, 4, 5)):
     return outs
 
 
-def pose_decoder(P, fa, fb):
+def pose_decoder(P, fa, fb, tag="pose"):
     """``(decoder::PoseDecoder)(features)`` -- src/pose_decoder.jl:23-32."""
-    sq = lambda f: F.relu(F.conv2d(f, P["pose.squeezer.weight"], P["pose.squeezer.bias"]))
-    y = torch.cat([sq(fa), sq(fb)], dim=1)
-    y = F.relu(F.conv2d(y, P["pose.conv1.weight"], P["pose.conv1.bias"], padding=1))
-    y = F.relu(F.conv2d(y, P["pose.conv2.weight"], P["pose.conv2.bias"], padding=1))
+    sq = lambda f, k: _relu(F.conv2d(f, P["pose.squeezer.weight"], P["pose.squeezer.bias"]), tag + k)
+    y = torch.cat([sq(fa, ".sqa"), sq(fb, ".sqb")], dim=1)
+    y = _relu(F.conv2d(y, P["pose.conv1.weight"], P["pose.conv1.bias"], padding=1), tag + ".conv1")
+    y = _relu(F.conv2d(y, P["pose.conv2.weight"], P["pose.conv2.bias"], padding=1), tag + ".conv2")
     y = F.conv2d(y, P["pose.conv3.weight"], P["pose.conv3.bias"])
     pose = 1e-2 * y.mean(dim=(2, 3))                               # [N,6]
     return pose[:, 0:3], pose[:, 3:6]
@@ -472,12 +516,12 @@ def model_forward(P, x, source_ids=(1, 3), target_id=2, arch=18, scale_levels=(2
     feats = [f.reshape(N, L, *f.shape[1:]) for f in feats]
     disps = depth_decoder(P, [f[:, target_id - 1] for f in feats], scale_levels)
     poses = []
-    for i in source_ids:                                           # eval_poses, src/model.jl:57-70
+    for j, i in enumerate(source_ids):                             # eval_poses, src/model.jl:57-70
         if i < target_id:
             fa, fb = feats[-1][:, i - 1], feats[-1][:, target_id - 1]
         else:
             fa, fb = feats[-1][:, target_id - 1], feats[-1][:, i - 1]
-        poses.append(pose_decoder(P, fa, fb))
+        poses.append(pose_decoder(P, fa, fb, tag=f"pose{j}"))
     return disps, poses
 
 

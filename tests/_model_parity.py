@@ -26,10 +26,12 @@ def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7):
     torch.cuda.synchronize()
     g = {"loss": loss.item(), "tail_loss": tail["loss"].item(), "disps": [d.cpu() for d in disps],
          "pose": pose.cpu(), "grad": model.grad.cpu(), "sel": tail["vis_sel"].cpu()}
+    g["decisions"] = gpu_decisions(model, N, arch)
     spec = O.param_spec(arch, C, (2, 3, 4, 5))
     flat = model.flat.detach().double().cpu().clone().requires_grad_(True)
     P = O.unflatten(flat, spec)
-    d_o, p_o = O.model_forward(P, x, arch=arch)
+    with O.forced_decisions(g["decisions"]):
+        d_o, p_o = O.model_forward(P, x, arch=arch)
     cache_o = O.TrainCache(K=K, invK=invK)
     par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
     forced = [g["sel"][s].unsqueeze(1).long() for s in range(4)]
@@ -50,7 +52,33 @@ def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7):
     return g, o, errs
 
 
-def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=None, sel=None):
+def gpu_decisions(model, N, arch=18, L=3):
+    """The GPU forward's branch decisions (ReLU masks, max-pool argmax) in the oracle's layout
+    (encoder batch n-major; pose per source pair) for O.forced_decisions."""
+    from oracle import md2_oracle as O
+    t = {k: v.cpu() for k, v in model._last.debug_tensors().items()}
+
+    def nmajor(v):   # frame-major [L*N, ...] -> n-major [N*L, ...]
+        return v.reshape(L, N, *v.shape[1:]).transpose(0, 1).reshape(L * N, *v.shape[1:])
+
+    d = {"stem": nmajor(t["stem.out"] > 0), "maxpool": nmajor(t["maxpool.arg"])}
+    for si, nb in enumerate(O.RESNET_LAYERS[arch]):
+        for bi in range(nb):
+            q = f"layer{si + 1}.{bi}"
+            d[f"encoder.{q}.out"] = nmajor(t[q + ".out"] > 0)
+            if q + ".relu1" in t:
+                d[f"encoder.{q}.relu1"] = nmajor(t[q + ".relu1"] > 0)
+    sq = t["pose.sq"] > 0
+    for j in range(2):                       # pair j = frames (j, j+1), GPU pairs [jN, (j+1)N)
+        d[f"pose{j}.sqa"] = sq[j * N:(j + 1) * N]
+        d[f"pose{j}.sqb"] = sq[(j + 1) * N:(j + 2) * N]
+        d[f"pose{j}.conv1"] = t["pose.conv1"][j * N:(j + 1) * N] > 0
+        d[f"pose{j}.conv2"] = t["pose.conv2"][j * N:(j + 1) * N] > 0
+    return d
+
+
+def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=None, sel=None,
+                      decisions=None):
     """Per-tensor gradient error of the SAME oracle run in fp32 vs fp64 (the fp32 noise floor)."""
     x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
     K, invK = D.intrinsics(W, H)
@@ -59,7 +87,8 @@ def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=
     for dt in (torch.float64, torch.float32):
         f = flat.to(dt).clone().requires_grad_(True)
         P = O.unflatten(f, spec)
-        d_o, p_o = O.model_forward(P, x.to(dt), arch=arch)
+        with O.forced_decisions(decisions or {}):
+            d_o, p_o = O.model_forward(P, x.to(dt), arch=arch)
         cache_o = O.TrainCache(K=K.to(dt), invK=invK.to(dt))
         par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
         forced = [s.unsqueeze(1).long() for s in sel]

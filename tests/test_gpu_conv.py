@@ -27,6 +27,23 @@ CASES = [
     ((6, 512, 4, 13), 256, 1, 1, 0, False, "relu", True),        # pose squeezer
     ((2, 8, 2, 3), 4, 3, 1, 1, True, "elu", True),               # reflect on a 2x3 map
     ((3, 5, 9, 11), 7, 3, 2, 1, False, "relu", True),            # ragged everything
+    # tap-major K order (channels % 16 == 0): reflect borders, CW = 16/32/64 wgrad tap blocks,
+    # stride-2 dgrad phases, 1x1/2 with few channels
+    ((2, 16, 2, 4), 16, 3, 1, 1, True, "elu", True),             # reflect, every pixel a border
+    ((2, 32, 4, 5), 32, 3, 1, 1, True, "elu", True),             # reflect, mixed border waves
+    ((2, 48, 8, 12), 64, 3, 1, 1, False, "relu", True),          # Cin 48 -> CW 16
+    ((2, 32, 9, 13), 16, 3, 2, 1, False, None, False),           # stride-2 dgrad, Cout 16
+    ((2, 16, 7, 9), 32, 1, 2, 0, False, None, False),            # 1x1/2, 16 channels
+    ((2, 64, 6, 10), 48, 3, 1, 1, True, "elu", True),            # reflect, CW 64, Cout 48
+    # the model-parity configuration (6 frames of 64x128): tiny deep maps
+    ((6, 64, 16, 32), 64, 3, 1, 1, False, None, False),          # layer1
+    ((6, 64, 16, 32), 128, 3, 2, 1, False, None, False),         # layer2.0.conv1
+    ((6, 128, 8, 16), 256, 3, 2, 1, False, None, False),         # layer3.0.conv1
+    ((6, 256, 4, 8), 512, 3, 2, 1, False, None, False),          # layer4.0.conv1
+    ((6, 512, 2, 4), 512, 3, 1, 1, False, None, False),          # layer4 3x3 on 2x4
+    ((6, 256, 4, 8), 512, 1, 2, 0, False, None, False),          # layer4 downsample
+    ((2, 512, 2, 4), 256, 3, 1, 1, True, "elu", True),           # branch1.c1 reflect 2x4
+    ((4, 512, 2, 4), 256, 3, 1, 1, False, "relu", True),         # pose conv1 on 2x4
 ]
 
 

@@ -26,7 +26,8 @@ def test_model_train_loss_parity(strict):
     for a, b in zip(g["disps"], o["disps"]):
         assert D.rel_err(a, b) < 1e-5
     assert D.rel_err(g["pose"], o["pose"]) < 1e-5
-    floor = oracle_fp32_floor(strict=strict, flat=_flat(), sel=[s for s in g["sel"]])
+    floor = oracle_fp32_floor(strict=strict, flat=_flat(), sel=[s for s in g["sel"]],
+                              decisions=g["decisions"])
     tier = 2e-4 if strict else 1e-2
     bad = {k: (v, floor[k]) for k, v in errs.items() if v > max(4 * floor[k], tier)}
     assert not bad, bad
@@ -95,3 +96,58 @@ def test_eval_disparity_parity():
     ref = O.eval_disparity(P, x)
     for a, b in zip(got, ref):
         assert D.rel_err(a.cpu(), b) < 1e-5
+
+
+@pytest.mark.parametrize("arch", [18])
+def test_encoder_layers_parity(arch):
+    """Every encoder layer of the GPU forward vs fp64 torch evaluated on the GPU's OWN input to
+    that layer (md2_model_debug_tensor): conv outputs, BN(+residual)+ReLU, max-pool.  Catches
+    wiring errors that train-mode BN would hide from the final outputs (a per-channel affine
+    error in a conv output cancels in the forward but not in the backward)."""
+    import torch.nn.functional as F
+    import md2hip
+    from oracle import md2_oracle as O
+    N, C, H, W = 2, 3, 64, 128
+    x = D.triplets(N, C, H, W, seed=7)
+    enc = md2hip.ResNet(arch, in_channels=C)
+    model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
+                                                  embedding_levels=0),
+                         md2hip.PoseDecoder(enc.stages[-1]), seed=42)
+    K, invK = D.intrinsics(W, H)
+    cache = md2hip.TrainCache(K=K.numpy(), invK=invK.numpy())
+    params = md2hip.Params(target_size=(W, H), batch_size=N, automasking=False)
+    md2hip.train_loss(model, x.float().cuda().contiguous(), None, cache, params)
+    t = {k: v.double().cpu() for k, v in model._last.debug_tensors().items()}
+    P = O.unflatten(model.flat.detach().double().cpu(), O.param_spec(arch, C, (2, 3, 4, 5)))
+
+    def bn(y, name):
+        return F.batch_norm(y, None, None, P[name + ".gamma"], P[name + ".beta"], training=True,
+                            eps=1e-5)
+
+    errs = {}
+    frames = x.float().double().transpose(0, 1).reshape(3 * N, C, H, W)   # frame-major batch
+    errs["stem.y"] = D.rel_err(t["stem.y"], F.conv2d(frames, P["encoder.stem.conv.weight"], stride=2, padding=3))
+    errs["stem.out"] = D.rel_err(t["stem.out"], F.relu(bn(t["stem.y"], "encoder.stem.bn")))
+    errs["maxpool.out"] = D.rel_err(t["maxpool.out"], F.max_pool2d(t["stem.out"], 3, 2, 1))
+    cur = t["maxpool.out"]
+    for si, nblocks in enumerate(O.RESNET_LAYERS[arch]):
+        for bi in range(nblocks):
+            q, p = f"layer{si + 1}.{bi}", f"encoder.layer{si + 1}.{bi}"
+            stride = 2 if (bi == 0 and si > 0) else 1
+            errs[q + ".conv1.y"] = D.rel_err(t[q + ".conv1.y"], F.conv2d(cur, P[p + ".conv1.weight"], stride=stride, padding=1))
+            errs[q + ".relu1"] = D.rel_err(t[q + ".relu1"], F.relu(bn(t[q + ".conv1.y"], p + ".bn1")))
+            errs[q + ".conv2.y"] = D.rel_err(t[q + ".conv2.y"], F.conv2d(t[q + ".relu1"], P[p + ".conv2.weight"], padding=1))
+            if q + ".down.y" in t:
+                errs[q + ".down.y"] = D.rel_err(t[q + ".down.y"], F.conv2d(cur, P[p + ".down.weight"], stride=2))
+                res = bn(t[q + ".down.y"], p + ".down_bn")
+            else:
+                res = cur
+            errs[q + ".out"] = D.rel_err(t[q + ".out"], F.relu(bn(t[q + ".conv2.y"], p + ".bn2") + res))
+            cur = t[q + ".out"]
+    sq = F.relu(F.conv2d(cur, P["pose.squeezer.weight"], P["pose.squeezer.bias"]))
+    errs["pose.sq"] = D.rel_err(t["pose.sq"], sq)
+    pin = torch.cat([t["pose.sq"][:2 * N], t["pose.sq"][N:]], 1)   # pairs (q, q + N)
+    errs["pose.conv1"] = D.rel_err(t["pose.conv1"], F.relu(F.conv2d(pin, P["pose.conv1.weight"], P["pose.conv1.bias"], padding=1)))
+    errs["pose.conv2"] = D.rel_err(t["pose.conv2"], F.relu(F.conv2d(t["pose.conv1"], P["pose.conv2.weight"], P["pose.conv2.bias"], padding=1)))
+    bad = {k: v for k, v in errs.items() if v > 1e-5}
+    assert not bad, bad
