@@ -48,12 +48,8 @@ def parse():
 
 def synthetic_batch(batch, height, width, rank, device):
     """Uniform [0,1) triplets keyed by GLOBAL sample index (GPU-count invariant shards)."""
-    import torch
-    xs = []
-    for i in range(batch):
-        g = torch.Generator().manual_seed(1234 + rank * batch + i)
-        xs.append(torch.rand(3, 3, height, width, generator=g))
-    return torch.stack(xs, 0).to(device).contiguous()
+    from md2hip.dist import synthetic_triplets
+    return synthetic_triplets(batch, height, width, rank * batch, device)
 
 
 def cpu_baseline(args, seconds):
@@ -90,6 +86,21 @@ def cpu_baseline(args, seconds):
             "sample": f"{n} full train step(s) at batch {B} {W}x{H} (fp32 torch-CPU oracle, after 1 warm-up)"}
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel set from the newest committed PMC profile
+    (tools/profile_round.sh + tools/prof_summary.py: separate FETCH_SIZE / WRITE_SIZE passes,
+    FETCH doubled per the gfx950 note).  PMC cannot run inside the timed bench."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f).get("traffic")
+    if not t:
+        return None, None
+    return round(t["bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+
+
 def main():
     args = parse()
     import torch
@@ -107,6 +118,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     import md2hip
+    import md2hip.dist
     B, H, W = args.batch, args.height, args.width
     enc = md2hip.ResNet(args.arch, in_channels=3)
     model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
@@ -119,17 +131,10 @@ def main():
     x = synthetic_batch(B, H, W, rank, dev)
     ex = model.executor(tuple(x.shape), cache, params)
     loss_buf = torch.empty(1, dtype=torch.float32, device=dev)
+    comm = md2hip.dist.GradAllReduce()
 
     def step():
-        ex.forward_loss(x, None, loss=loss_buf)
-        handles = []
-        for k in range(ex.nseg):
-            off, ln = ex.backward_segment(k)
-            if world > 1:
-                handles.append(dist.all_reduce(model.grad[off:off + ln], async_op=True))
-        for h in handles:
-            h.wait()
-        opt.update(model, grad_scale=1.0 / world)
+        md2hip.dist.train_step(ex, model, opt, x, comm, loss=loss_buf)
 
     def barrier():
         if world > 1:
@@ -182,9 +187,11 @@ def main():
         if prof:
             ms, flop, n = prof["conv3x3_encoder"]
             ach = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-            out["roofline"] = {"bound": "mfma", "kernel": "conv_px/conv_wgrad implicit-GEMM (encoder 3x3, fwd+dgrad+wgrad)",
+            traffic, tsrc = pmc_traffic()
+            out["roofline"] = {"bound": "mfma", "kernel": "conv_px/conv_wgrad implicit-GEMM, zero-padded 3x3 convs (encoder+pose; fwd+dgrad+wgrad+split-K reduce)",
                                "achieved": round(ach, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                               "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                               "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
+                               "traffic_source": tsrc,
                                "launches": n, "algorithmic_flop_per_step": flop, "kernel_ms_per_step": round(ms, 4)}
             ms, byt, n = prof["photometric"]
             gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0

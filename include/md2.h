@@ -170,7 +170,8 @@ int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, f
 /* device pointers of the last forward: disparities per level and poses [2*batch][6] */
 int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose);
 /* HIP-event profiling of the hot kernels on the model's stream (bench roofline): categories
- * 0 = encoder 3x3 convs (fwd/dgrad/wgrad, work = algorithmic FLOP), 1 = other convs,
+ * 0 = zero-padded 3x3 convs (encoder + pose decoder; fwd/dgrad/wgrad incl. their split-K
+ * reductions, work = algorithmic FLOP), 1 = other convs,
  * 2 = fused warp+SSIM photometric kernel (work = algorithmic HBM bytes).
  * out[cat*3 + {0,1,2}] = {total ms, total work, launches}; read() clears. */
 #define MD2_PROF_NCAT 3

@@ -429,6 +429,7 @@ class Model {
     need_ws(p1, 2 * N, wsn, true);
     MD2_TRY(make_conv(p2, spec.p2, h4, w4, true, wsn));
     need_ws(p2, 2 * N, wsn, true);
+    p1.cat = p2.cat = PROF_CONV3_ENC;     // zero-padded 3x3 like the encoder's (same kernels)
     MD2_TRY(alloc(&sqo, (long)B * 256 * hw4));
     MD2_TRY(alloc(&d_sq, (long)B * 256 * hw4));
     MD2_TRY(alloc(&pc1, 2L * N * 256 * hw4));
