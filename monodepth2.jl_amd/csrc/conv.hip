@@ -154,7 +154,28 @@ struct ConvArgs {
   // which implements the zero padding of the gathers without branches)
   uint32_t A_bytes, b0_bytes, b1_bytes;
   uint32_t HW4, HoWo4;   // channel strides in bytes (scalar soffset steps of the tap-major gathers)
+  // stride-2 dgrad by output-parity class (tap-major only): the N axis enumerates the input
+  // pixels (ph_y0 + 2j, ph_x0 + 2i) of one class (fd_pix / fd_row are the class extents) and K
+  // runs over that class's taps ph_taps[0..ntaps) only
+  int ph_y0, ph_x0;
+  int ph_taps[16];       // <= ceil(7/2)^2 taps per class
 };
+
+// (image, pixel-in-plane) of N-axis element nn for fwd / dgrad outputs
+__device__ __forceinline__ void out_pixel(const ConvArgs& a, bool phase, long nn, int& img, long& pix,
+                                          long& plane) {
+  img = (int)fdiv((uint32_t)nn, a.fd_pix);
+  const long r = nn - (long)img * a.fd_pix.d;
+  if (phase) {
+    const int jy = (int)fdiv((uint32_t)r, a.fd_row);
+    const int jx = (int)(r - (long)jy * a.fd_row.d);
+    pix = (long)(a.ph_y0 + 2 * jy) * a.W + a.ph_x0 + 2 * jx;
+    plane = a.HW;
+  } else {
+    pix = r;
+    plane = a.fd_pix.d;
+  }
+}
 
 constexpr uint32_t OOB = 0x7ffffff0u;   // byte offset that is out of range for every tensor
 
@@ -220,7 +241,7 @@ __device__ __forceinline__ void store_out(const TensorOut& o, int m, int img, lo
 #include "conv_px.inc"
 
 // split-K reduction + epilogue for fwd / dgrad
-__global__ __launch_bounds__(256) void splitk_reduce_px_kernel(ConvArgs a, int splits) {
+__global__ __launch_bounds__(256) void splitk_reduce_px_kernel(ConvArgs a, int splits, int phase) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   const long total = (long)a.g.M * a.g.N;
   if (idx >= total) return;
@@ -228,9 +249,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_px_kernel(ConvArgs a, int s
   const long nn = idx - (long)m * a.g.N;
   float v = 0.f;
   for (int s = 0; s < splits; ++s) v += a.slab[(long)s * total + idx];
-  const int img = (int)fdiv((uint32_t)nn, a.fd_pix);
-  const long pix = nn - (long)img * a.fd_pix.d;
-  store_out(a.out, m, img, pix, a.fd_pix.d, v);
+  int img;
+  long pix, plane;
+  out_pixel(a, phase != 0, nn, img, pix, plane);
+  store_out(a.out, m, img, pix, plane, v);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -590,6 +612,11 @@ Plan plan_px(int M, long N, int K) {
     p.tile = T32x256; p.BM = 32; p.BN = 256;
   }
   p.BK = 16;
+  if (K <= 0) {                // a parity class without taps: the kernel only writes zeros
+    p.splits = 1;
+    p.kper = p.BK;
+    return p;
+  }
   const long tiles = (long)cdiv(M, p.BM) * cdiv(N, p.BN);
   int splits = 1;
   while (tiles * splits * 2 <= TARGET_BLOCKS && K / (splits * 2) >= 8 * p.BK) splits *= 2;
@@ -706,7 +733,8 @@ int launch_px(const ConvShape& s, ConvArgs& a, const Plan& p, ConvWorkspace ws, 
   if (rc) return rc;
   if (p.splits > 1) {
     const long total = (long)a.g.M * a.g.N;
-    hipLaunchKernelGGL(splitk_reduce_px_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a, p.splits);
+    hipLaunchKernelGGL(splitk_reduce_px_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a, p.splits,
+                       (int)(MODE == 1 && s.stride == 2 && conv_tap_major(s, 1)));
     MD2_LAUNCH_CHECK();
   }
   return MD2_OK;
@@ -732,6 +760,25 @@ int launch_w(int cw, const ConvArgs& a, dim3 grid, hipStream_t st) {
   return MD2_OK;
 }
 
+// stride-2 dgrad output-parity class (cy, cx): input pixels iy = y0 + 2j with (iy + pad) % 2 ==
+// cy receive exactly the taps kh % 2 == cy (same for columns)
+struct PhaseClass {
+  int y0, x0, Hc, Wc, ntaps;
+  int taps[16];
+};
+
+PhaseClass phase_class(const ConvShape& s, int cy, int cx) {
+  PhaseClass c{};
+  c.y0 = (cy + s.pad) & 1;
+  c.x0 = (cx + s.pad) & 1;
+  c.Hc = (s.H - c.y0 + 1) / 2;
+  c.Wc = (s.W - c.x0 + 1) / 2;
+  static_assert(sizeof(c.taps) / sizeof(c.taps[0]) >= 16, "taps of a 7x7 class");
+  for (int kh = cy; kh < s.KH; kh += 2)
+    for (int kw = cx; kw < s.KW; kw += 2) c.taps[c.ntaps++] = kh * s.KW + kw;
+  return c;
+}
+
 }  // namespace
 
 bool conv_tap_major(const ConvShape& s, int mode) {
@@ -755,6 +802,16 @@ size_t conv_fwd_workspace(const ConvShape& s) {
 }
 
 size_t conv_dgrad_workspace(const ConvShape& s) {
+  if (s.stride == 2 && conv_tap_major(s, 1)) {
+    size_t b = 0;
+    for (int cls = 0; cls < 4; ++cls) {
+      const PhaseClass c = phase_class(s, cls >> 1, cls & 1);
+      const long N = (long)s.N * c.Hc * c.Wc;
+      const Plan p = plan_px(s.Cin, N, c.ntaps * s.Cout);
+      if (p.splits > 1) b = std::max(b, (size_t)p.splits * s.Cin * N * sizeof(float));
+    }
+    return b;
+  }
   const long N = (long)s.N * s.H * s.W;
   const Plan p = plan_px(s.Cin, N, s.Cout * s.KH * s.KW);
   return p.splits > 1 ? (size_t)p.splits * s.Cin * N * sizeof(float) : 0;
@@ -832,6 +889,24 @@ int conv_dgrad(const ConvShape& s, const float* dy, const float* wpacked_d, cons
   MD2_CHECK_ARG((long)s.N * s.Cout * s.Ho * s.Wo * 4 < (long)OOB, "conv_dgrad: tensor exceeds 2 GB");
   a.b0_bytes = (uint32_t)((long)s.N * s.Cout * s.Ho * s.Wo * 4);
   a.b1_bytes = 0;
+  if (s.stride == 2 && conv_tap_major(s, 1)) {
+    // four dense GEMMs over the output-parity classes, each with only its own taps
+    for (int cls = 0; cls < 4; ++cls) {
+      const PhaseClass c = phase_class(s, cls >> 1, cls & 1);
+      if (c.Hc <= 0 || c.Wc <= 0 || (c.ntaps == 0 && dx.accumulate)) continue;
+      ConvArgs ac = a;
+      ac.ph_y0 = c.y0;
+      ac.ph_x0 = c.x0;
+      for (int t = 0; t < 16; ++t) ac.ph_taps[t] = t < c.ntaps ? c.taps[t] : 0;
+      ac.g.N = (long)s.N * c.Hc * c.Wc;
+      ac.g.K = c.ntaps * s.Cout;
+      ac.fd_pix = make_fastdiv((uint32_t)(c.Hc * c.Wc));
+      ac.fd_row = make_fastdiv((uint32_t)c.Wc);
+      const Plan p = plan_px(ac.g.M, ac.g.N, ac.g.K);
+      MD2_TRY(launch_px<1>(s, ac, p, ws, st));
+    }
+    return MD2_OK;
+  }
   const Plan p = plan_px(a.g.M, a.g.N, a.g.K);
   return launch_px<1>(s, a, p, ws, st);
 }

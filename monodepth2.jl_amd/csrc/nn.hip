@@ -10,22 +10,41 @@ namespace md2 {
 int bn_parts(int C, long N, long HW) {
   long total = N * HW;
   int parts = (int)std::max(1L, std::min(1024L / std::max(1, C) + 1, total / 2048 + 1));
-  return std::min(parts, 256);
+  return (int)std::min<long>(std::min(parts, 256), std::max(1L, N));   // parts split images
 }
 
-// one block per (channel, part); sums over a contiguous slice of the N*HW elements
+// Element index helpers: every activation here is < 2^31 elements (checked on the host), so
+// indices are 32-bit and divisions by runtime extents use magic numbers (FastDiv).
+static FastDiv fd(long d) { return make_fastdiv((uint32_t)d); }
+static int check_u31(long n) {
+  MD2_CHECK_ARG(n >= 0 && n < (1L << 31), "tensor larger than 2^31 elements");
+  return MD2_OK;
+}
+
+// One block per (channel c, image group p): the group's images x HW elements of channel c,
+// walked as a flat range (float4 units when HW % 4 == 0); fp64 accumulation.
+template <bool VEC>
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ y, int C,
-                                                               long HW, long total, int parts,
-                                                               double* __restrict__ part) {
+                                                               int HW, int N, int parts,
+                                                               FastDiv fdu, double* __restrict__ part) {
   __shared__ double red[8];
   const int c = blockIdx.x, p = blockIdx.y;
-  const long beg = total * p / parts, end = total * (p + 1) / parts;
+  const int i0 = (int)((long)N * p / parts), i1 = (int)((long)N * (p + 1) / parts);
+  const int U = VEC ? HW / 4 : HW;                 // units per image
+  const uint32_t nu = (uint32_t)(i1 - i0) * U;
   double s = 0.0, ss = 0.0;
-  for (long e = beg + threadIdx.x; e < end; e += 256) {
-    const long img = e / HW, pix = e - img * HW;
-    const double v = y[(img * C + c) * HW + pix];
-    s += v;
-    ss += v * v;
+  for (uint32_t e = threadIdx.x; e < nu; e += 256) {
+    const uint32_t im = fdiv(e, fdu), k = e - im * U;
+    const long base = ((long)(i0 + im) * C + c) * HW;
+    if (VEC) {
+      const float4 v = *reinterpret_cast<const float4*>(y + base + 4 * k);
+      s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+      ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    } else {
+      const double v = y[base + k];
+      s += v;
+      ss += v * v;
+    }
   }
   s = wave_sum_d(s);
   ss = wave_sum_d(ss);
@@ -64,9 +83,17 @@ __global__ void bn_stats_final_kernel(const double* __restrict__ part, int C, in
 
 int bn_stats(const float* y, int N, int C, long HW, float eps, float momentum, float* mean,
              float* invstd, float* run_mean, float* run_var, BNStatsWs ws, hipStream_t st) {
+  MD2_TRY(check_u31((long)N * C * HW));
+  MD2_CHECK_ARG(ws.parts >= 1 && ws.parts <= N, "bn_stats: parts must split the images");
   const long total = (long)N * HW;
-  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(C, ws.parts), dim3(256), 0, st, y, C, HW, total,
-                     ws.parts, ws.partials);
+  const int vec = HW % 4 == 0;
+  const FastDiv fdu = fd(vec ? HW / 4 : HW);
+  if (vec)
+    hipLaunchKernelGGL(bn_stats_partial_kernel<true>, dim3(C, ws.parts), dim3(256), 0, st, y, C,
+                       (int)HW, N, ws.parts, fdu, ws.partials);
+  else
+    hipLaunchKernelGGL(bn_stats_partial_kernel<false>, dim3(C, ws.parts), dim3(256), 0, st, y, C,
+                       (int)HW, N, ws.parts, fdu, ws.partials);
   MD2_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_stats_final_kernel, dim3(cdiv(C, 64)), dim3(64), 0, st, ws.partials, C,
                      ws.parts, total, eps, momentum, mean, invstd, run_mean, run_var);
@@ -74,13 +101,18 @@ int bn_stats(const float* y, int N, int C, long HW, float eps, float momentum, f
   return MD2_OK;
 }
 
-// float4 over [N][C][HW] with HW % 4 == 0 (all encoder maps) or scalar fallback
+// channel of element unit u (float4 or scalar units): plane = u / U, c = plane % C
+__device__ __forceinline__ int unit_channel(uint32_t u, const FastDiv& fdU, const FastDiv& fdC) {
+  const uint32_t plane = fdiv(u, fdU);
+  return (int)(plane - fdiv(plane, fdC) * fdC.d);
+}
+
 template <bool VEC>
-__global__ __launch_bounds__(256) void bn_apply_kernel(BNApply p, float* __restrict__ out, int C,
-                                                       long HW, long n) {
-  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * (VEC ? 4 : 1);
-  if (i >= n) return;
-  const int c = (int)((i / HW) % C);
+__global__ __launch_bounds__(256) void bn_apply_kernel(BNApply p, float* __restrict__ out,
+                                                       uint32_t nu, FastDiv fdU, FastDiv fdC) {
+  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= nu) return;
+  const int c = unit_channel(u, fdU, fdC);
   const float sc = p.gamma[c] * p.invstd[c], sh = p.beta[c] - p.mean[c] * sc;
   float sc2 = 0.f, sh2 = 0.f;
   if (p.y2) {
@@ -88,15 +120,16 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BNApply p, float* __restr
     sh2 = p.beta2[c] - p.mean2[c] * sc2;
   }
   if (VEC) {
+    const long i = 4L * u;
     float4 v = *reinterpret_cast<const float4*>(p.y + i);
     float r[4] = {v.x * sc + sh, v.y * sc + sh, v.z * sc + sh, v.w * sc + sh};
     if (p.y2) {
-      const float4 u = *reinterpret_cast<const float4*>(p.y2 + i);
-      r[0] += u.x * sc2 + sh2; r[1] += u.y * sc2 + sh2; r[2] += u.z * sc2 + sh2; r[3] += u.w * sc2 + sh2;
+      const float4 q = *reinterpret_cast<const float4*>(p.y2 + i);
+      r[0] += q.x * sc2 + sh2; r[1] += q.y * sc2 + sh2; r[2] += q.z * sc2 + sh2; r[3] += q.w * sc2 + sh2;
     }
     if (p.res) {
-      const float4 u = *reinterpret_cast<const float4*>(p.res + i);
-      r[0] += u.x; r[1] += u.y; r[2] += u.z; r[3] += u.w;
+      const float4 q = *reinterpret_cast<const float4*>(p.res + i);
+      r[0] += q.x; r[1] += q.y; r[2] += q.z; r[3] += q.w;
     }
     if (p.relu) {
 #pragma unroll
@@ -104,41 +137,64 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BNApply p, float* __restr
     }
     *reinterpret_cast<float4*>(out + i) = make_float4(r[0], r[1], r[2], r[3]);
   } else {
-    float r = p.y[i] * sc + sh;
-    if (p.y2) r += p.y2[i] * sc2 + sh2;
-    if (p.res) r += p.res[i];
+    float r = p.y[u] * sc + sh;
+    if (p.y2) r += p.y2[u] * sc2 + sh2;
+    if (p.res) r += p.res[u];
     if (p.relu) r = fmaxf(r, 0.f);
-    out[i] = r;
+    out[u] = r;
   }
 }
 
 int bn_apply(const BNApply& p, float* out, int N, int C, long HW, hipStream_t st) {
   const long n = (long)N * C * HW;
+  MD2_TRY(check_u31(n));
   if (HW % 4 == 0) {
-    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st, p, out, C, HW, n);
+    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st, p, out,
+                       (uint32_t)(n / 4), fd(HW / 4), fd(C));
   } else {
-    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st, p, out, C, HW, n);
+    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st, p, out,
+                       (uint32_t)n, fd(HW), fd(C));
   }
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
 
+template <bool VEC>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
-    const float* __restrict__ mean, const float* __restrict__ invstd, int C, long HW, long total,
-    int parts, double* __restrict__ part) {
+    const float* __restrict__ mean, const float* __restrict__ invstd, int C, int HW, int N,
+    int parts, FastDiv fdu, double* __restrict__ part) {
   __shared__ double red[8];
   const int c = blockIdx.x, p = blockIdx.y;
-  const long beg = total * p / parts, end = total * (p + 1) / parts;
+  const int i0 = (int)((long)N * p / parts), i1 = (int)((long)N * (p + 1) / parts);
+  const int U = VEC ? HW / 4 : HW;
+  const uint32_t nu = (uint32_t)(i1 - i0) * U;
   const float mu = mean[c], is = invstd[c];
   double sg = 0.0, sgx = 0.0;
-  for (long e = beg + threadIdx.x; e < end; e += 256) {
-    const long img = e / HW, pix = e - img * HW;
-    const long idx = (img * C + c) * HW + pix;
-    float g = dout[idx];
-    if (mask && !(mask[idx] > 0.f)) g = 0.f;
-    sg += g;
-    sgx += (double)g * (double)((y[idx] - mu) * is);
+  for (uint32_t e = threadIdx.x; e < nu; e += 256) {
+    const uint32_t im = fdiv(e, fdu), k = e - im * U;
+    const long base = ((long)(i0 + im) * C + c) * HW;
+    if (VEC) {
+      const long i = base + 4 * k;
+      float4 g = *reinterpret_cast<const float4*>(dout + i);
+      if (mask) {
+        const float4 m = *reinterpret_cast<const float4*>(mask + i);
+        if (!(m.x > 0.f)) g.x = 0.f;
+        if (!(m.y > 0.f)) g.y = 0.f;
+        if (!(m.z > 0.f)) g.z = 0.f;
+        if (!(m.w > 0.f)) g.w = 0.f;
+      }
+      const float4 v = *reinterpret_cast<const float4*>(y + i);
+      sg += (double)g.x + (double)g.y + (double)g.z + (double)g.w;
+      sgx += (double)g.x * (double)((v.x - mu) * is) + (double)g.y * (double)((v.y - mu) * is) +
+             (double)g.z * (double)((v.z - mu) * is) + (double)g.w * (double)((v.w - mu) * is);
+    } else {
+      const long i = base + k;
+      float g = dout[i];
+      if (mask && !(mask[i] > 0.f)) g = 0.f;
+      sg += g;
+      sgx += (double)g * (double)((y[i] - mu) * is);
+    }
   }
   sg = wave_sum_d(sg);
   sgx = wave_sum_d(sgx);
@@ -170,9 +226,16 @@ __global__ void bn_bwd_final_kernel(const double* __restrict__ part, int C, int 
 int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, const float* mean,
                   const float* invstd, int N, int C, long HW, float* dgamma, float* dbeta,
                   BNStatsWs ws, hipStream_t st) {
-  const long total = (long)N * HW;
-  hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(C, ws.parts), dim3(256), 0, st, dout, mask_out, y,
-                     mean, invstd, C, HW, total, ws.parts, ws.partials);
+  MD2_TRY(check_u31((long)N * C * HW));
+  MD2_CHECK_ARG(ws.parts >= 1 && ws.parts <= N, "bn_bwd: parts must split the images");
+  const int vec = HW % 4 == 0;
+  const FastDiv fdu = fd(vec ? HW / 4 : HW);
+  if (vec)
+    hipLaunchKernelGGL(bn_bwd_partial_kernel<true>, dim3(C, ws.parts), dim3(256), 0, st, dout,
+                       mask_out, y, mean, invstd, C, (int)HW, N, ws.parts, fdu, ws.partials);
+  else
+    hipLaunchKernelGGL(bn_bwd_partial_kernel<false>, dim3(C, ws.parts), dim3(256), 0, st, dout,
+                       mask_out, y, mean, invstd, C, (int)HW, N, ws.parts, fdu, ws.partials);
   MD2_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 64)), dim3(64), 0, st, ws.partials, C,
                      ws.parts, dgamma, dbeta);
@@ -180,25 +243,57 @@ int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, cons
   return MD2_OK;
 }
 
+template <bool VEC>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ dgamma,
-    const float* __restrict__ dbeta, int C, long HW, long n, float invL, float* __restrict__ dy,
-    float* __restrict__ dres, int dres_acc) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int c = (int)((i / HW) % C);
-  float g = dout[i];
-  if (mask && !(mask[i] > 0.f)) g = 0.f;
-  const float is = invstd[c];
-  const float xh = (y[i] - mean[c]) * is;
-  dy[i] = gamma[c] * is * (g - dbeta[c] * invL - xh * dgamma[c] * invL);
-  if (dres) {
-    if (dres_acc)
-      dres[i] += g;
-    else
-      dres[i] = g;
+    const float* __restrict__ dbeta, uint32_t nu, FastDiv fdU, FastDiv fdC, float invL,
+    float* __restrict__ dy, float* __restrict__ dres, int dres_acc) {
+  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= nu) return;
+  const int c = unit_channel(u, fdU, fdC);
+  const float is = invstd[c], mu = mean[c];
+  const float k0 = gamma[c] * is, db = dbeta[c] * invL, dg = dgamma[c] * invL;
+  if (VEC) {
+    const long i = 4L * u;
+    float g[4];
+    {
+      const float4 t = *reinterpret_cast<const float4*>(dout + i);
+      g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
+    }
+    if (mask) {
+      const float4 m = *reinterpret_cast<const float4*>(mask + i);
+      if (!(m.x > 0.f)) g[0] = 0.f;
+      if (!(m.y > 0.f)) g[1] = 0.f;
+      if (!(m.z > 0.f)) g[2] = 0.f;
+      if (!(m.w > 0.f)) g[3] = 0.f;
+    }
+    const float4 v = *reinterpret_cast<const float4*>(y + i);
+    const float yv[4] = {v.x, v.y, v.z, v.w};
+    float r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = k0 * (g[k] - db - (yv[k] - mu) * is * dg);
+    *reinterpret_cast<float4*>(dy + i) = make_float4(r[0], r[1], r[2], r[3]);
+    if (dres) {
+      float4 o = make_float4(g[0], g[1], g[2], g[3]);
+      if (dres_acc) {
+        const float4 q = *reinterpret_cast<const float4*>(dres + i);
+        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+      }
+      *reinterpret_cast<float4*>(dres + i) = o;
+    }
+  } else {
+    float g = dout[u];
+    if (mask && !(mask[u] > 0.f)) g = 0.f;
+    const float xh = (y[u] - mu) * is;
+    dy[u] = k0 * (g - db - xh * dg);
+    if (dres) {
+      if (dres_acc)
+        dres[u] += g;
+      else
+        dres[u] = g;
+    }
   }
 }
 
@@ -207,9 +302,16 @@ int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const
                  const float* dbeta, int N, int C, long HW, float* dy, float* dres,
                  int dres_accumulate, hipStream_t st) {
   const long n = (long)N * C * HW;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dout, mask_out, y,
-                     mean, invstd, gamma, dgamma, dbeta, C, HW, n, 1.f / (float)((long)N * HW), dy,
-                     dres, dres_accumulate);
+  MD2_TRY(check_u31(n));
+  const float invL = 1.f / (float)((long)N * HW);
+  if (HW % 4 == 0)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st, dout,
+                       mask_out, y, mean, invstd, gamma, dgamma, dbeta, (uint32_t)(n / 4), fd(HW / 4),
+                       fd(C), invL, dy, dres, dres_accumulate);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st, dout,
+                       mask_out, y, mean, invstd, gamma, dgamma, dbeta, (uint32_t)n, fd(HW), fd(C),
+                       invL, dy, dres, dres_accumulate);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -220,12 +322,12 @@ int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restrict__ x, int H, int W,
                                                           float* __restrict__ y,
                                                           unsigned char* __restrict__ arg, int Ho,
-                                                          int Wo, long n) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+                                                          FastDiv fdWo, FastDiv fdHo, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const int ow = (int)(i % Wo), oh = (int)((i / Wo) % Ho);
-  const long plane = i / ((long)Ho * Wo);
-  const float* p = x + plane * H * W;
+  const uint32_t r = fdiv(i, fdWo), plane = fdiv(r, fdHo);
+  const int ow = (int)(i - r * fdWo.d), oh = (int)(r - plane * fdHo.d);
+  const float* p = x + (long)plane * H * W;
   float best = -INFINITY;
   int bi = 0;
 #pragma unroll
@@ -247,26 +349,29 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restric
   arg[i] = (unsigned char)bi;
 }
 
+// gather: input (ih, iw) is tap kh = ih + 1 - 2 oh of at most two output rows (same for columns)
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ dy,
                                                           const unsigned char* __restrict__ arg,
-                                                          int H, int W, int Ho, int Wo,
-                                                          float* __restrict__ dx, long n) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+                                                          int H, int Ho, int Wo, FastDiv fdW,
+                                                          FastDiv fdH, float* __restrict__ dx,
+                                                          uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const int iw = (int)(i % W), ih = (int)((i / W) % H);
-  const long plane = i / ((long)H * W);
-  const float* g = dy + plane * Ho * Wo;
-  const unsigned char* a = arg + plane * Ho * Wo;
+  const uint32_t r = fdiv(i, fdW), plane = fdiv(r, fdH);
+  const int iw = (int)(i - r * fdW.d), ih = (int)(r - plane * fdH.d);
+  const long ob = (long)plane * Ho * Wo;
+  const int oh1 = (ih + 1) >> 1, ow1 = (iw + 1) >> 1;     // tap 0/1; oh1-1 has tap 2/3
   float s = 0.f;
-  const int oh_lo = max(0, (ih - 1 + 1) / 2), oh_hi = min(Ho - 1, (ih + 1) / 2);
-  const int ow_lo = max(0, (iw - 1 + 1) / 2), ow_hi = min(Wo - 1, (iw + 1) / 2);
-  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-    const int kh = ih - (oh * 2 - 1);
-    if (kh < 0 || kh > 2) continue;
-    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-      const int kw = iw - (ow * 2 - 1);
-      if (kw < 0 || kw > 2) continue;
-      if (a[oh * Wo + ow] == kh * 3 + kw) s += g[oh * Wo + ow];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int oh = oh1 - a, kh = ih + 1 - 2 * oh;
+    if (oh < 0 || oh >= Ho || kh > 2) continue;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int ow = ow1 - b, kw = iw + 1 - 2 * ow;
+      if (ow < 0 || ow >= Wo || kw > 2) continue;
+      const long o = ob + oh * Wo + ow;
+      if (arg[o] == kh * 3 + kw) s += dy[o];
     }
   }
   dx[i] = s;
@@ -275,7 +380,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
 int maxpool_fwd(const float* x, int N, int C, int H, int W, float* y, unsigned char* arg, int Ho,
                 int Wo, hipStream_t st) {
   const long n = (long)N * C * Ho * Wo;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, x, H, W, y, arg, Ho, Wo, n);
+  MD2_TRY(check_u31((long)N * C * H * W));
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, x, H, W, y, arg, Ho,
+                     fd(Wo), fd(Ho), (uint32_t)n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -283,7 +390,9 @@ int maxpool_fwd(const float* x, int N, int C, int H, int W, float* y, unsigned c
 int maxpool_bwd(const float* dy, const unsigned char* arg, int N, int C, int H, int W, int Ho,
                 int Wo, float* dx, hipStream_t st) {
   const long n = (long)N * C * H * W;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, arg, H, W, Ho, Wo, dx, n);
+  MD2_TRY(check_u31(n));
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, arg, H, Ho, Wo,
+                     fd(W), fd(H), dx, (uint32_t)n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -299,14 +408,14 @@ __device__ __forceinline__ void src_idx(int o, float r, int in, int& i0, int& i1
 }
 
 __global__ __launch_bounds__(256) void upsample2_fwd_kernel(const float* __restrict__ x, int h,
-                                                            int w, float ry, float rx,
-                                                            float* __restrict__ y, long n) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+                                                            int w, float ry, float rx, FastDiv fdW2,
+                                                            FastDiv fdH2, float* __restrict__ y,
+                                                            uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const int W2 = 2 * w, H2 = 2 * h;
-  const int ox = (int)(i % W2), oy = (int)((i / W2) % H2);
-  const long plane = i / ((long)H2 * W2);
-  const float* p = x + plane * h * w;
+  const uint32_t r = fdiv(i, fdW2), plane = fdiv(r, fdH2);
+  const int ox = (int)(i - r * fdW2.d), oy = (int)(r - plane * fdH2.d);
+  const float* p = x + (long)plane * h * w;
   int y0, y1, x0, x1;
   float fy, fx;
   src_idx(oy, ry, h, y0, y1, fy);
@@ -324,14 +433,15 @@ __device__ __forceinline__ float up_w(int o, int j, float r, int in) {
 
 // gather adjoint: input pixel (iy, ix) collects the output pixels whose 2x2 stencil touches it
 __global__ __launch_bounds__(256) void upsample2_bwd_kernel(const float* __restrict__ dy, int h,
-                                                            int w, float ry, float rx,
-                                                            float* __restrict__ dx, long n) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+                                                            int w, float ry, float rx, FastDiv fdw,
+                                                            FastDiv fdh, float* __restrict__ dx,
+                                                            uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const int W2 = 2 * w, H2 = 2 * h;
-  const int ix = (int)(i % w), iy = (int)((i / w) % h);
-  const long plane = i / ((long)h * w);
-  const float* g = dy + plane * H2 * W2;
+  const uint32_t r = fdiv(i, fdw), plane = fdiv(r, fdh);
+  const int ix = (int)(i - r * fdw.d), iy = (int)(r - plane * fdh.d);
+  const float* g = dy + (long)plane * H2 * W2;
   // outputs o with floor(o*r) in {i-1, i}:  o in [(i-1)/r, (i+1)/r]
   const int ylo = (h == 1) ? 0 : max(0, (int)floorf((float)(iy - 1) / ry) - 1);
   const int yhi = (h == 1) ? H2 - 1 : min(H2 - 1, (int)ceilf((float)(iy + 1) / ry) + 1);
@@ -355,16 +465,18 @@ static inline float up_ratio(int in, int out) { return out > 1 ? (float)(in - 1)
 
 int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStream_t st) {
   const long n = (long)N * C * 4 * h * w;
+  MD2_TRY(check_u31(n));
   hipLaunchKernelGGL(upsample2_fwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, x, h, w,
-                     up_ratio(h, 2 * h), up_ratio(w, 2 * w), y, n);
+                     up_ratio(h, 2 * h), up_ratio(w, 2 * w), fd(2 * w), fd(2 * h), y, (uint32_t)n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
 
 int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStream_t st) {
   const long n = (long)N * C * h * w;
+  MD2_TRY(check_u31(4 * n));
   hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, h, w,
-                     up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx, n);
+                     up_ratio(h, 2 * h), up_ratio(w, 2 * w), fd(w), fd(h), dx, (uint32_t)n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -406,12 +518,12 @@ int pose_head_fwd(const float* x, int Q, int C, long HW, const float* w, const f
 
 __global__ __launch_bounds__(256) void pose_head_dx_kernel(const float* __restrict__ dpose, int C,
                                                            long HW, const float* __restrict__ w,
-                                                           float* __restrict__ dx, long n) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+                                                           FastDiv fdHW, FastDiv fdC,
+                                                           float* __restrict__ dx, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const long qc = i / HW;
-  const int c = (int)(qc % C);
-  const long q = qc / C;
+  const uint32_t qc = fdiv(i, fdHW), q = fdiv(qc, fdC);
+  const int c = (int)(qc - q * fdC.d);
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < 6; ++k) s += dpose[q * 6 + k] * w[(long)k * C + c];
@@ -439,7 +551,9 @@ __global__ __launch_bounds__(256) void pose_head_dw_kernel(const float* __restri
 int pose_head_bwd(const float* dpose, int Q, int C, long HW, const float* w, const float* means,
                   float* dx, float* dw, float* db, hipStream_t st) {
   const long n = (long)Q * C * HW;
-  hipLaunchKernelGGL(pose_head_dx_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dpose, C, HW, w, dx, n);
+  MD2_TRY(check_u31(n));
+  hipLaunchKernelGGL(pose_head_dx_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dpose, C, HW, w,
+                     fd(HW), fd(C), dx, (uint32_t)n);
   MD2_LAUNCH_CHECK();
   hipLaunchKernelGGL(pose_head_dw_kernel, dim3(cdiv(6 * C, 256)), dim3(256), 0, st, dpose, Q, C,
                      means, dw, db);
@@ -464,21 +578,26 @@ int axpy(float* y, const float* x, long n, hipStream_t st) {
 
 // pose pairs q = s*N + n read (sq[q], sq[q+N]) (src/model.jl:65-70 in frame-major order):
 // dsq[b] = (b < 2N ? dpin[b][0:C] : 0) + (b >= N ? dpin[b-N][C:2C] : 0)
-__global__ __launch_bounds__(256) void pair_grad_kernel(const float* __restrict__ dpin, int N, int C,
-                                                        long HW, float* __restrict__ dsq, long n) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(256) void pair_grad_kernel(const float* __restrict__ dpin, int N,
+                                                        FastDiv fdper, float* __restrict__ dsq,
+                                                        uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const long per = (long)C * HW;
-  const long b = i / per, r = i - b * per;
+  const long per = fdper.d;
+  const uint32_t b = fdiv(i, fdper);
+  const long r = i - (long)b * per;
   float s = 0.f;
-  if (b < 2 * N) s += dpin[b * 2 * per + r];
-  if (b >= N) s += dpin[(b - N) * 2 * per + per + r];
+  const long bl = b;
+  if (bl < 2L * N) s += dpin[bl * 2 * per + r];
+  if (bl >= N) s += dpin[(bl - N) * 2 * per + per + r];
   dsq[i] = s;
 }
 
 int pair_grad_gather(const float* dpin, int N, int C, long HW, float* dsq, hipStream_t st) {
   const long n = 3L * N * C * HW;
-  hipLaunchKernelGGL(pair_grad_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dpin, N, C, HW, dsq, n);
+  MD2_TRY(check_u31(2 * n));
+  hipLaunchKernelGGL(pair_grad_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dpin, N, fd((long)C * HW),
+                     dsq, (uint32_t)n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
