@@ -591,9 +591,18 @@ __global__ __launch_bounds__(256) void act_backward_kernel(const float* __restri
 // ---------------------------------------------------------------------------------------------
 namespace {
 
-constexpr int TARGET_BLOCKS = 768;   // ~3 blocks per CU on 256 CUs
+constexpr int TARGET_BLOCKS = 1536;  // ~6 blocks (waves per SIMD) per CU on 256 CUs
 
-enum TileCfg { T128x128 = 0, T64x256 = 1, T32x256 = 2 };
+enum TileCfg { T128x128 = 0, T64x256 = 1, T32x256 = 2, T64x128 = 3, T128x64 = 4, T64x64 = 5, T32x128 = 6 };
+const int TILE_BM[] = {128, 64, 32, 64, 128, 64, 32};
+const int TILE_BN[] = {128, 256, 256, 128, 64, 64, 128};
+
+// debugging / tuning overrides of the planner (read once): MD2_PX_TILE=<TileCfg>,
+// MD2_PX_TARGET=<target blocks for the split-K choice>
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
 
 struct Plan {
   int tile;
@@ -603,14 +612,18 @@ struct Plan {
 };
 
 Plan plan_px(int M, long N, int K) {
+  // Small tiles, many blocks: at B=12 the GEMMs are ~0.5 chip of 128x128 tiles; 64x64 tiles
+  // (30 VGPR + 16 AGPR, 8 waves/SIMD) with ~1536 blocks keep 4-6 waves per SIMD in flight and
+  // ran 10-50% faster than 128x128 / 64x256 on every encoder shape (tools/sweep_px.sh, r01).
+  static const int tile_override = env_int("MD2_PX_TILE", -1);
+  static const int target = env_int("MD2_PX_TARGET", TARGET_BLOCKS);
   Plan p{};
-  if (M > 64) {
-    p.tile = T128x128; p.BM = 128; p.BN = 128;
-  } else if (M > 32) {
-    p.tile = T64x256; p.BM = 64; p.BN = 256;
-  } else {
-    p.tile = T32x256; p.BM = 32; p.BN = 256;
-  }
+  p.tile = M > 32 ? T64x64 : T32x128;
+  if (tile_override >= 0 && tile_override <= T32x128 &&
+      (M > 32 || tile_override == T32x256 || tile_override == T32x128))
+    p.tile = tile_override;
+  p.BM = TILE_BM[p.tile];
+  p.BN = TILE_BN[p.tile];
   p.BK = 16;
   if (K <= 0) {                // a parity class without taps: the kernel only writes zeros
     p.splits = 1;
@@ -619,54 +632,67 @@ Plan plan_px(int M, long N, int K) {
   }
   const long tiles = (long)cdiv(M, p.BM) * cdiv(N, p.BN);
   int splits = 1;
-  while (tiles * splits * 2 <= TARGET_BLOCKS && K / (splits * 2) >= 8 * p.BK) splits *= 2;
+  while (tiles * splits * 2 <= target && K / (splits * 2) >= 8 * p.BK) splits *= 2;
   p.kper = (int)round_up(cdiv(K, splits), p.BK);
   p.splits = cdiv(K, p.kper);
   return p;
 }
 
-// wgrad: n_tiles = column tiles (tap-major: tap groups x channel blocks)
-Plan plan_w(int M, long n_tiles_128, long n_tiles_256, long K) {
-  Plan p{};
-  if (M <= 32) {          // decoder 16/32-channel layers: do not pad Cout to 64
-    p.tile = 1; p.BM = 32; p.BN = 256; p.BK = 32;
-  } else {
-    p.tile = 0; p.BM = 64; p.BN = 128; p.BK = 32;
-  }
-  const long tiles = (long)cdiv(M, p.BM) * (p.tile == 1 ? n_tiles_256 : n_tiles_128);
-  long splits = std::max(1L, (long)512 / tiles);   // 2 blocks/CU resident
-  splits = std::min(splits, std::max(1L, K / (8 * p.BK)));
-  p.kper = (int)round_up((K + splits - 1) / splits, p.BK);
-  p.splits = (int)((K + p.kper - 1) / p.kper);
-  return p;
-}
+// wgrad tiles (BM x BN, 4 waves as WM x WN); columns are tap-major (tap groups x CW channels)
+enum WTileCfg { W64x128 = 0, W32x256 = 1, W64x64 = 2, W32x128 = 3 };
+const int WT_BM[] = {64, 32, 64, 32};
+const int WT_BN[] = {128, 256, 64, 128};
 
-// channels per tap block of the tap-major wgrad: largest of 128/64/32/16 dividing Cin and the
-// concat split
-int wgrad_cw(const ConvShape& s, int c0) {
+struct WPlan {
+  int tile, BM, BN;
+  int cw;          // channels per tap block (0: channel-major kernel)
+  long ntiles_n;   // column tiles
+  int splits, kper;
+};
+
+// channels per tap block of the tap-major wgrad: largest of 128/64/32/16 (<= BN) dividing Cin and
+// the concat split
+int wgrad_cw(const ConvShape& s, int c0, int BN) {
   for (int cw = 128; cw >= 16; cw /= 2)
-    if (s.Cin % cw == 0 && (c0 >= s.Cin || c0 % cw == 0)) return cw;
+    if (cw <= BN && s.Cin % cw == 0 && (c0 >= s.Cin || c0 % cw == 0)) return cw;
   return 0;
 }
 
-struct WTiles {
-  int cw;          // 0: channel-major kernel
-  long n128, n256; // column tiles for BN = 128 / 256
-};
-
-WTiles wgrad_tiles(const ConvShape& s, int c0) {
-  WTiles t{};
+WPlan plan_wgrad(const ConvShape& s, int c0) {
+  static const int tile_override = env_int("MD2_W_TILE", -1);
+  static const int target = env_int("MD2_W_TARGET", 0);
+  WPlan p{};
+  const int M = s.Cout;
   const int KK = s.KH * s.KW;
-  const long N = (long)s.Cin * KK;
-  t.cw = conv_tap_major(s, 2) ? wgrad_cw(s, c0) : 0;
-  if (t.cw) {
-    t.n128 = (long)cdiv(KK, std::max(1, 128 / t.cw)) * (s.Cin / t.cw);
-    t.n256 = (long)cdiv(KK, 256 / t.cw) * (s.Cin / t.cw);
+  auto ntiles = [&](int tile, int& cw) {
+    cw = conv_tap_major(s, 2) ? wgrad_cw(s, c0, WT_BN[tile]) : 0;
+    const long nt = cw ? (long)cdiv(KK, WT_BN[tile] / cw) * (s.Cin / cw) : cdiv((long)s.Cin * KK, WT_BN[tile]);
+    return (long)cdiv(M, WT_BM[tile]) * nt;
+  };
+  // M <= 32: 32x128 (1024 blocks); else 64x128 with split-K to ~512 blocks, or 64x64 when the
+  // grid is already >= 256 tiles without splitting (tools/sweep_w.sh, r01)
+  int tgt = 512;
+  if (M <= 32) {
+    p.tile = W32x128;
+    tgt = 1024;
   } else {
-    t.n128 = cdiv(N, 128);
-    t.n256 = cdiv(N, 256);
+    int cw;
+    p.tile = ntiles(W64x128, cw) >= 256 ? W64x64 : W64x128;
+    if (p.tile == W64x64) tgt = 1024;
   }
-  return t;
+  if (tile_override >= 0 && tile_override <= W32x128) p.tile = tile_override;
+  if (target > 0) tgt = target;
+  p.BM = WT_BM[p.tile];
+  p.BN = WT_BN[p.tile];
+  const long tiles = ntiles(p.tile, p.cw);
+  p.ntiles_n = tiles / cdiv(M, p.BM);
+  const long K = (long)s.N * s.Ho * s.Wo;
+  const int BK = 32;
+  long splits = std::max(1L, (long)tgt / tiles);
+  splits = std::min(splits, std::max(1L, K / (8 * BK)));
+  p.kper = (int)round_up((K + splits - 1) / splits, BK);
+  p.splits = (int)((K + p.kper - 1) / p.kper);
+  return p;
 }
 
 void fill_common(ConvArgs& a, const ConvShape& s) {
@@ -728,6 +754,10 @@ int launch_px(const ConvShape& s, ConvArgs& a, const Plan& p, ConvWorkspace ws, 
   switch (p.tile) {
     case T128x128: rc = launch_px_tile<MODE, 128, 128, 2, 2>(s, a, tap, grid, st); break;
     case T64x256: rc = launch_px_tile<MODE, 64, 256, 1, 4>(s, a, tap, grid, st); break;
+    case T64x128: rc = launch_px_tile<MODE, 64, 128, 2, 2>(s, a, tap, grid, st); break;
+    case T128x64: rc = launch_px_tile<MODE, 128, 64, 2, 2>(s, a, tap, grid, st); break;
+    case T64x64: rc = launch_px_tile<MODE, 64, 64, 2, 2>(s, a, tap, grid, st); break;
+    case T32x128: rc = launch_px_tile<MODE, 32, 128, 1, 4>(s, a, tap, grid, st); break;
     default: rc = launch_px_tile<MODE, 32, 256, 1, 4>(s, a, tap, grid, st); break;
   }
   if (rc) return rc;
@@ -740,6 +770,13 @@ int launch_px(const ConvShape& s, ConvArgs& a, const Plan& p, ConvWorkspace ws, 
   return MD2_OK;
 }
 
+template <int BM, int BN, int WM, int WN, int KS, int SS, int RR, int CW>
+void launch_w_cw(const ConvArgs& a, dim3 grid, hipStream_t st) {
+  if constexpr (CW <= BN)
+    hipLaunchKernelGGL((conv_wgrad_tap_kernel<BM, BN, 32, WM, WN, KS, KS, SS, RR, CW>), grid,
+                       dim3(256), 0, st, a);
+}
+
 template <int BM, int BN, int WM, int WN, int KS, int SS, int RR>
 int launch_w(int cw, const ConvArgs& a, dim3 grid, hipStream_t st) {
   switch (cw) {
@@ -747,13 +784,10 @@ int launch_w(int cw, const ConvArgs& a, dim3 grid, hipStream_t st) {
       hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, 32, WM, WN, KS, KS, SS, RR>), grid, dim3(256), 0,
                          st, a);
       break;
-#define MD2_W_CW(CW)                                                                               \
-  case CW:                                                                                         \
-    hipLaunchKernelGGL((conv_wgrad_tap_kernel<BM, BN, 32, WM, WN, KS, KS, SS, RR, CW>), grid,       \
-                       dim3(256), 0, st, a);                                                       \
-    break;
-      MD2_W_CW(16) MD2_W_CW(32) MD2_W_CW(64) MD2_W_CW(128)
-#undef MD2_W_CW
+    case 16: launch_w_cw<BM, BN, WM, WN, KS, SS, RR, 16>(a, grid, st); break;
+    case 32: launch_w_cw<BM, BN, WM, WN, KS, SS, RR, 32>(a, grid, st); break;
+    case 64: launch_w_cw<BM, BN, WM, WN, KS, SS, RR, 64>(a, grid, st); break;
+    case 128: launch_w_cw<BM, BN, WM, WN, KS, SS, RR, 128>(a, grid, st); break;
     default: return MD2_ENOTSUP;
   }
   MD2_LAUNCH_CHECK();
@@ -820,8 +854,7 @@ size_t conv_dgrad_workspace(const ConvShape& s) {
 static size_t wgrad_ws_bytes(const ConvShape& s, int c0) {
   const long K = (long)s.N * s.Ho * s.Wo;
   const long Nc = (long)s.Cin * s.KH * s.KW;
-  const WTiles t = wgrad_tiles(s, c0);
-  const Plan p = plan_w(s.Cout, t.n128, t.n256, K);
+  const WPlan p = plan_wgrad(s, c0);
   const size_t groups = (size_t)std::min(p.splits, WRED_GROUPS);
   return ((size_t)p.splits + groups) * s.Cout * Nc * sizeof(float) +
          (size_t)s.Cout * bias_parts(s.Cout, K) * sizeof(float) + 256;
@@ -916,8 +949,8 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
   MD2_TRY(check_shape(s));
   MD2_CHECK_ARG(x.p0 && dy && dw, "conv_wgrad pointers");
   MD2_CHECK_ARG(x.c0 >= s.Cin || x.p1 != nullptr, "conv_wgrad: second input tensor missing");
-  const WTiles wt = wgrad_tiles(s, x.c0);
-  const bool tap = wt.cw > 0;
+  const WPlan p = plan_wgrad(s, x.c0);
+  const bool tap = p.cw > 0;
   ConvArgs a{};
   fill_common(a, s);
   const long Kpix = (long)s.N * s.Ho * s.Wo;
@@ -942,7 +975,6 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
     a.b1_bytes = (uint32_t)(ext1 * 4);
     a.A_bytes = (uint32_t)(extd * 4);
   }
-  const Plan p = plan_w(a.g.M, wt.n128, wt.n256, Kpix);
   a.g.kper = p.kper;
   const size_t need = conv_wgrad_workspace(s);
   MD2_CHECK_ARG(ws.ptr && ws.bytes >= need, "conv_wgrad workspace too small");
@@ -951,14 +983,16 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
   const int groups = std::min(p.splits, WRED_GROUPS);
   float* part = a.slab + (long)p.splits * total;
   float* bpart = part + (long)groups * total;
-  dim3 grid((unsigned)(p.tile == 1 ? wt.n256 : wt.n128), cdiv(a.g.M, p.BM), p.splits);
+  dim3 grid((unsigned)p.ntiles_n, cdiv(a.g.M, p.BM), p.splits);
   int rc = MD2_ENOTSUP;
 #define MD2_W_CASE(KS, SS, RR)                                                                     \
   if (rc == MD2_ENOTSUP && s.KH == KS && s.stride == SS && s.reflect == RR) {                      \
-    if (p.tile == 1)                                                                               \
-      rc = launch_w<32, 256, 1, 4, KS, SS, RR>(wt.cw, a, grid, st);                                \
-    else                                                                                           \
-      rc = launch_w<64, 128, 2, 2, KS, SS, RR>(wt.cw, a, grid, st);                                \
+    switch (p.tile) {                                                                              \
+      case W32x256: rc = launch_w<32, 256, 1, 4, KS, SS, RR>(p.cw, a, grid, st); break;            \
+      case W64x64: rc = launch_w<64, 64, 2, 2, KS, SS, RR>(p.cw, a, grid, st); break;              \
+      case W32x128: rc = launch_w<32, 128, 1, 4, KS, SS, RR>(p.cw, a, grid, st); break;            \
+      default: rc = launch_w<64, 128, 2, 2, KS, SS, RR>(p.cw, a, grid, st); break;                 \
+    }                                                                                              \
   }
   MD2_CONV_COMBOS(MD2_W_CASE)
 #undef MD2_W_CASE

@@ -255,6 +255,7 @@ class Model {
 
   ~Model() {
     for (void* p : allocs) (void)hipFree(p);
+    for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
   }
 
   int alloc(float** p, size_t n) {
@@ -750,6 +751,14 @@ class Model {
     prof_end(e, c.cat, conv_flops(s), st);
     return MD2_OK;
   }
+  // filter and data gradient of one conv from the same dY.  (Running the filter gradient on a
+  // second stream overlapped them but each slowed by as much, and the cross-queue fork/join
+  // added ~1.3 ms/step of idle gaps: measured slower, so both stay on `st`.)
+  int conv_wd(RConv& c, int nimg, const TensorIn& in, const float* dy, float* dx, long dx_bs,
+              int acc, hipStream_t st, float* dx1 = nullptr, long dx1_bs = 0, int c0 = 1 << 30) {
+    MD2_TRY(conv_w(c, nimg, in, dy, st));
+    return conv_d(c, nimg, dy, dx, dx_bs, acc, st, dx1, dx1_bs, c0);
+  }
   int conv_d(RConv& c, int nimg, const float* dy, float* dx, long dx_bs, int acc, hipStream_t st,
              float* dx1 = nullptr, long dx1_bs = 0, int c0 = 1 << 30) {
     ConvShape s = c.s;
@@ -785,21 +794,19 @@ class Model {
     MD2_TRY(bn_bwd(last.bn, b.d_out, last.a, last.y, nimg, ohw, DY, b.down ? G : b.d_in, 0, st));
     if (b.down) {
       MD2_TRY(bn_bwd(b.dbn, G, nullptr, b.yd, nimg, ohw, DYD, nullptr, 0, st));
-      MD2_TRY(conv_w(b.dconv, nimg, tin(b.in, b.Cin, ihw), DYD, st));
-      MD2_TRY(conv_d(b.dconv, nimg, DYD, b.d_in, (long)b.Cin * ihw, 0, st));
+      MD2_TRY(conv_wd(b.dconv, nimg, tin(b.in, b.Cin, ihw), DYD, b.d_in, (long)b.Cin * ihw, 0, st));
     }
     for (int k = ns - 1; k >= 0; --k) {
       EncStage& e = b.st[k];
       const float* xin = k == 0 ? b.in : b.st[k - 1].a;
       const int cin = e.conv.p.cin;
       const long hin = (long)e.conv.s.H * e.conv.s.W;
-      MD2_TRY(conv_w(e.conv, nimg, tin(xin, cin, hin), DY, st));
       if (k > 0) {
-        MD2_TRY(conv_d(e.conv, nimg, DY, DA, (long)cin * hin, 0, st));
+        MD2_TRY(conv_wd(e.conv, nimg, tin(xin, cin, hin), DY, DA, (long)cin * hin, 0, st));
         EncStage& pe = b.st[k - 1];
         MD2_TRY(bn_bwd(pe.bn, DA, pe.a, pe.y, nimg, hin, DY, nullptr, 0, st));
       } else {
-        MD2_TRY(conv_d(e.conv, nimg, DY, b.d_in, (long)cin * hin, 1, st));
+        MD2_TRY(conv_wd(e.conv, nimg, tin(xin, cin, hin), DY, b.d_in, (long)cin * hin, 1, st));
       }
     }
     return MD2_OK;
@@ -811,19 +818,16 @@ class Model {
     MD2_TRY(pose_head_bwd(d_pose, 2 * N, 256, hw4, P(spec.p3.w), means, DPRE, Gd(spec.p3.w),
                           Gd(spec.p3.b), st));
     MD2_TRY(act_backward(pc2, DPRE, DPRE, 2L * N * 256 * hw4, ACT_RELU, st));
-    MD2_TRY(conv_w(p2, 2 * N, tin(pc1, 256, hw4), DPRE, st));
-    MD2_TRY(conv_d(p2, 2 * N, DPRE, d_pc1, 256 * hw4, 0, st));
+    MD2_TRY(conv_wd(p2, 2 * N, tin(pc1, 256, hw4), DPRE, d_pc1, 256 * hw4, 0, st));
     MD2_TRY(act_backward(pc1, d_pc1, d_pc1, 2L * N * 256 * hw4, ACT_RELU, st));
     TensorIn pin = tin(sqo, 256, hw4);
     pin.p1 = sqo + (long)N * 256 * hw4;
     pin.bs1 = 256 * hw4;
-    MD2_TRY(conv_w(p1, 2 * N, pin, d_pc1, st));
-    MD2_TRY(conv_d(p1, 2 * N, d_pc1, d_pin, 512 * hw4, 0, st));
+    MD2_TRY(conv_wd(p1, 2 * N, pin, d_pc1, d_pin, 512 * hw4, 0, st));
     MD2_TRY(pair_grad_gather(d_pin, N, 256, hw4, d_sq, st));
     MD2_TRY(act_backward(sqo, d_sq, d_sq, (long)B * 256 * hw4, ACT_RELU, st));
-    MD2_TRY(conv_w(sq, B, tin(feat[4], featC[4], hw4), d_sq, st));
     float* d_f4 = stages[3].back().d_out;
-    MD2_TRY(conv_d(sq, B, d_sq, d_f4, (long)featC[4] * hw4, 0, st));
+    MD2_TRY(conv_wd(sq, B, tin(feat[4], featC[4], hw4), d_sq, d_f4, (long)featC[4] * hw4, 0, st));
     // ---- DepthDecoder backward (reverse branch order)
     const int nb = (int)br.size();
     for (int i = nb - 1; i >= 0; --i) {
@@ -831,8 +835,7 @@ class Model {
       const long hw = (long)d.h * d.w, hw2 = 4 * hw;
       const int co = d.b.cout;
       if (d.head >= 0) {
-        MD2_TRY(conv_w(d.hc, N, tin(d.o2, co, hw2), d.d_head, st));
-        MD2_TRY(conv_d(d.hc, N, d.d_head, d.d_o2, co * hw2, i < nb - 1 ? 1 : 0, st));
+        MD2_TRY(conv_wd(d.hc, N, tin(d.o2, co, hw2), d.d_head, d.d_o2, co * hw2, i < nb - 1 ? 1 : 0, st));
       }
       MD2_TRY(act_backward(d.o2, d.d_o2, DPRE, (long)N * co * hw2, ACT_ELU, st));
       TensorIn in = tin(d.up, co, hw2);
@@ -845,8 +848,7 @@ class Model {
         dskip = d_skip[fi];
         skip_bs = (long)featC[fi] * hw2;
       }
-      MD2_TRY(conv_w(d.c2, N, in, DPRE, st));
-      MD2_TRY(conv_d(d.c2, N, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
+      MD2_TRY(conv_wd(d.c2, N, in, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
       MD2_TRY(upsample2_bwd(DUP, N, co, d.h, d.w, DO1, st));
       MD2_TRY(act_backward(d.o1, DO1, DO1, (long)N * co * hw, ACT_ELU, st));
       const float* xin;
@@ -864,8 +866,7 @@ class Model {
         dx = br[i - 1].d_o2;
         acc = 0;
       }
-      MD2_TRY(conv_w(d.c1, N, tin(xin, cin, hw), DO1, st));
-      MD2_TRY(conv_d(d.c1, N, DO1, dx, (long)cin * hw, acc, st));
+      MD2_TRY(conv_wd(d.c1, N, tin(xin, cin, hw), DO1, dx, (long)cin * hw, acc, st));
     }
     return MD2_OK;
   }
