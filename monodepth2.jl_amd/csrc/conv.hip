@@ -611,7 +611,7 @@ struct Plan {
   int kper;
 };
 
-Plan plan_px(int M, long N, int K) {
+Plan plan_px(int M, long N, int K, bool bk32_ok = false) {
   // Small tiles, many blocks: at B=12 the GEMMs are ~0.5 chip of 128x128 tiles; 64x64 tiles
   // (30 VGPR + 16 AGPR, 8 waves/SIMD) with ~1536 blocks keep 4-6 waves per SIMD in flight and
   // ran 10-50% faster than 128x128 / 64x256 on every encoder shape (tools/sweep_px.sh, r01).
@@ -624,7 +624,8 @@ Plan plan_px(int M, long N, int K) {
     p.tile = tile_override;
   p.BM = TILE_BM[p.tile];
   p.BN = TILE_BN[p.tile];
-  p.BK = 16;
+  static const int bk_override = env_int("MD2_PX_BK", 16);
+  p.BK = (bk_override == 32 && bk32_ok) ? 32 : 16;
   if (K <= 0) {                // a parity class without taps: the kernel only writes zeros
     p.splits = 1;
     p.kper = p.BK;
@@ -721,10 +722,13 @@ int check_shape(const ConvShape& s) {
 #define MD2_CONV_COMBOS(X) X(1, 1, 0) X(1, 2, 0) X(3, 1, 0) X(3, 1, 1) X(3, 2, 0) X(7, 2, 0)
 
 template <int MODE, int BM, int BN, int WM, int WN>
-int launch_px_tile(const ConvShape& s, const ConvArgs& a, bool tap, dim3 grid, hipStream_t st) {
+int launch_px_tile(const ConvShape& s, const ConvArgs& a, bool tap, int bk, dim3 grid, hipStream_t st) {
 #define MD2_PX_CASE(KS, SS, RR)                                                                  \
   if (s.KH == KS && s.stride == SS && s.reflect == RR) {                                         \
-    if (tap)                                                                                     \
+    if (tap && bk == 32)                                                                         \
+      hipLaunchKernelGGL((conv_px_kernel<MODE, 1, BM, BN, 32, WM, WN, KS, KS, SS, RR>), grid,    \
+                         dim3(256), 0, st, a);                                                   \
+    else if (tap)                                                                                \
       hipLaunchKernelGGL((conv_px_kernel<MODE, 1, BM, BN, 16, WM, WN, KS, KS, SS, RR>), grid,    \
                          dim3(256), 0, st, a);                                                   \
     else                                                                                         \
@@ -752,13 +756,13 @@ int launch_px(const ConvShape& s, ConvArgs& a, const Plan& p, ConvWorkspace ws, 
   const bool tap = conv_tap_major(s, MODE);
   int rc;
   switch (p.tile) {
-    case T128x128: rc = launch_px_tile<MODE, 128, 128, 2, 2>(s, a, tap, grid, st); break;
-    case T64x256: rc = launch_px_tile<MODE, 64, 256, 1, 4>(s, a, tap, grid, st); break;
-    case T64x128: rc = launch_px_tile<MODE, 64, 128, 2, 2>(s, a, tap, grid, st); break;
-    case T128x64: rc = launch_px_tile<MODE, 128, 64, 2, 2>(s, a, tap, grid, st); break;
-    case T64x64: rc = launch_px_tile<MODE, 64, 64, 2, 2>(s, a, tap, grid, st); break;
-    case T32x128: rc = launch_px_tile<MODE, 32, 128, 1, 4>(s, a, tap, grid, st); break;
-    default: rc = launch_px_tile<MODE, 32, 256, 1, 4>(s, a, tap, grid, st); break;
+    case T128x128: rc = launch_px_tile<MODE, 128, 128, 2, 2>(s, a, tap, p.BK, grid, st); break;
+    case T64x256: rc = launch_px_tile<MODE, 64, 256, 1, 4>(s, a, tap, p.BK, grid, st); break;
+    case T64x128: rc = launch_px_tile<MODE, 64, 128, 2, 2>(s, a, tap, p.BK, grid, st); break;
+    case T128x64: rc = launch_px_tile<MODE, 128, 64, 2, 2>(s, a, tap, p.BK, grid, st); break;
+    case T64x64: rc = launch_px_tile<MODE, 64, 64, 2, 2>(s, a, tap, p.BK, grid, st); break;
+    case T32x128: rc = launch_px_tile<MODE, 32, 128, 1, 4>(s, a, tap, p.BK, grid, st); break;
+    default: rc = launch_px_tile<MODE, 32, 256, 1, 4>(s, a, tap, p.BK, grid, st); break;
   }
   if (rc) return rc;
   if (p.splits > 1) {
@@ -831,7 +835,8 @@ bool conv_tap_major(const ConvShape& s, int mode) {
 
 size_t conv_fwd_workspace(const ConvShape& s) {
   const long N = (long)s.N * s.Ho * s.Wo;
-  const Plan p = plan_px(s.Cout, N, s.Cin * s.KH * s.KW);
+  const Plan p = plan_px(s.Cout, N, s.Cin * s.KH * s.KW);   // BK does not change the split count
+
   return p.splits > 1 ? (size_t)p.splits * s.Cout * N * sizeof(float) : 0;
 }
 
@@ -897,7 +902,8 @@ int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const 
     a.b0_bytes = (uint32_t)(ext0 * 4);
     a.b1_bytes = (uint32_t)(ext1 * 4);
   }
-  const Plan p = plan_px(a.g.M, a.g.N, a.g.K);
+  const bool bk32 = conv_tap_major(s, 0) && s.Cin % 32 == 0 && (x.c0 >= s.Cin || x.c0 % 32 == 0);
+  const Plan p = plan_px(a.g.M, a.g.N, a.g.K, bk32);
   return launch_px<0>(s, a, p, ws, st);
 }
 
@@ -935,12 +941,12 @@ int conv_dgrad(const ConvShape& s, const float* dy, const float* wpacked_d, cons
       ac.g.K = c.ntaps * s.Cout;
       ac.fd_pix = make_fastdiv((uint32_t)(c.Hc * c.Wc));
       ac.fd_row = make_fastdiv((uint32_t)c.Wc);
-      const Plan p = plan_px(ac.g.M, ac.g.N, ac.g.K);
+      const Plan p = plan_px(ac.g.M, ac.g.N, ac.g.K, s.Cout % 32 == 0);
       MD2_TRY(launch_px<1>(s, ac, p, ws, st));
     }
     return MD2_OK;
   }
-  const Plan p = plan_px(a.g.M, a.g.N, a.g.K);
+  const Plan p = plan_px(a.g.M, a.g.N, a.g.K, conv_tap_major(s, 1) && s.Cout % 32 == 0);
   return launch_px<1>(s, a, p, ws, st);
 }
 
