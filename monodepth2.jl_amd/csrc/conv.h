@@ -52,6 +52,8 @@ struct ConvWorkspace {
 // multiple of the chunk.  Otherwise (the 3-channel stem, 1-channel disparity heads) the order is
 // channel-major k = c*KK + tap.  mode: 0 forward (C = Cin), 1 dgrad (C = Cout), 2 wgrad columns.
 bool conv_tap_major(const ConvShape& s, int mode);
+// forward (mode 0) / dgrad (mode 1) run the k-contiguous kernel with packed layout 1
+bool conv_px2_used(const ConvShape& s, int mode);
 
 // packed operand sizes (elements) -- weights are repacked K-major with zero padding
 size_t conv_fwd_packed_elems(const ConvShape& s);
@@ -65,6 +67,7 @@ struct PackJob {
   float* out;
   int mode;            // 0 forward, 1 dgrad
   int tap;             // tap-major K order (conv_tap_major)
+  int layout;          // 0: [Kpad][Mpad]; 1: [Kpad/16][Mpad][16] (k-contiguous chunks, conv_px2)
   int Cout, Cin, KK, Kpad, Mpad;
   long block_begin;    // first 256-element block of this job in the batched grid
 };

@@ -41,7 +41,17 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // forward:  Wt[k][m] = W[m][c][tap]   ([Kpad][Mpad]);   dgrad: Wd[k][ci] = W[co][ci][tap]
 // ([Kdpad][Cinpad]); k = tap*C + c (tap-major) or c*KK + tap, C = Cin (forward) / Cout (dgrad)
 __device__ __forceinline__ float pack_value(const PackJob& j, long idx) {
-  const int k = (int)(idx / j.Mpad), m = (int)(idx % j.Mpad);
+  int k, m;
+  if (j.layout) {
+    const long chunk = (long)j.Mpad * 16;
+    const int kc = (int)(idx / chunk);
+    const int r = (int)(idx - kc * chunk);
+    m = r >> 4;
+    k = kc * 16 + (r & 15);
+  } else {
+    k = (int)(idx / j.Mpad);
+    m = (int)(idx % j.Mpad);
+  }
   const int C = j.mode == 0 ? j.Cin : j.Cout;     // reduction channels
   const int Mr = j.mode == 0 ? j.Cout : j.Cin;    // rows
   if (k >= C * j.KK || m >= Mr) return 0.f;
@@ -75,6 +85,7 @@ PackJob conv_pack_job(const ConvShape& s, int mode, const float* w, float* out) 
   j.out = out;
   j.mode = mode;
   j.tap = conv_tap_major(s, mode) ? 1 : 0;
+  j.layout = conv_px2_used(s, mode) ? 1 : 0;
   j.Cout = s.Cout;
   j.Cin = s.Cin;
   j.KK = s.KH * s.KW;
@@ -239,6 +250,7 @@ __device__ __forceinline__ void store_out(const TensorOut& o, int m, int img, lo
 }
 
 #include "conv_px.inc"
+#include "conv_px2.inc"
 
 // split-K reduction + epilogue for fwd / dgrad
 __global__ __launch_bounds__(256) void splitk_reduce_px_kernel(ConvArgs a, int splits, int phase) {
@@ -620,7 +632,7 @@ Plan plan_px(int M, long N, int K, bool bk32_ok = false) {
   Plan p{};
   p.tile = M > 32 ? T64x64 : T32x128;
   if (tile_override >= 0 && tile_override <= T32x128 &&
-      (M > 32 || tile_override == T32x256 || tile_override == T32x128))
+      ((M > 32 && TILE_BM[tile_override] >= 64) || (M <= 32 && TILE_BM[tile_override] == 32)))
     p.tile = tile_override;
   p.BM = TILE_BM[p.tile];
   p.BN = TILE_BN[p.tile];
@@ -723,8 +735,21 @@ int check_shape(const ConvShape& s) {
 
 template <int MODE, int BM, int BN, int WM, int WN>
 int launch_px_tile(const ConvShape& s, const ConvArgs& a, bool tap, int bk, dim3 grid, hipStream_t st) {
+  const bool v2 = conv_px2_used(s, MODE);
 #define MD2_PX_CASE(KS, SS, RR)                                                                  \
   if (s.KH == KS && s.stride == SS && s.reflect == RR) {                                         \
+    if constexpr (BM >= 64 && BN % 64 == 0) {                                                    \
+      if (v2) {                                                                                  \
+        hipLaunchKernelGGL((conv_px2_kernel<MODE, BM, BN, WM, WN, KS, KS, SS, RR>), grid,        \
+                           dim3(256), 0, st, a);                                                 \
+        MD2_LAUNCH_CHECK();                                                                      \
+        return MD2_OK;                                                                           \
+      }                                                                                          \
+    }                                                                                            \
+    if (v2) {                                                                                    \
+      set_error("conv: k-contiguous kernel needs a tile with BM >= 64");                         \
+      return MD2_EINVAL;                                                                         \
+    }                                                                                            \
     if (tap && bk == 32)                                                                         \
       hipLaunchKernelGGL((conv_px_kernel<MODE, 1, BM, BN, 32, WM, WN, KS, KS, SS, RR>), grid,    \
                          dim3(256), 0, st, a);                                                   \
@@ -818,6 +843,17 @@ PhaseClass phase_class(const ConvShape& s, int cy, int cx) {
 }
 
 }  // namespace
+
+// the k-contiguous kernel (conv_px2.inc) runs every tap-major fwd / dgrad with M > 32 (tiles with
+// BM >= 64); MD2_PX_V2=0 selects the previous kernel (A/B)
+bool conv_px2_used(const ConvShape& s, int mode) {
+  static const int v2 = [] {
+    const char* e = getenv("MD2_PX_V2");
+    return e ? atoi(e) : 1;
+  }();
+  if (!v2 || mode > 1 || !conv_tap_major(s, mode)) return false;
+  return (mode == 0 ? s.Cout : s.Cin) > 32;
+}
 
 bool conv_tap_major(const ConvShape& s, int mode) {
   // MD2_CONV_CHANNEL_MAJOR=<bitmask of modes> forces the channel-major order (debugging)
