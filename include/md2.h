@@ -119,6 +119,20 @@ int md2_act_backward(const float* out, const float* dout, float* dpre, long long
                      void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Pooling / resampling layers of the networks, [n][c][h][w] planes.
+ * MaxPool((3,3), pad=1, stride=2) of the ResNet.jl stem: y [n][c][ho][wo] with
+ * ho = (h+1)/2, wo = (w+1)/2, arg = window index kh*3+kw of the first maximum (uint8, kept for
+ * the pullback).  upsample_bilinear(x, (2,2)), align_corners (src/depth_decoder.jl:18-19):
+ * y [n][c][2h][2w]; the backward is its exact adjoint dx [n][c][h][w].
+ * ---------------------------------------------------------------------------------------- */
+int md2_maxpool3s2_fwd(const float* x, int n, int c, int h, int w, float* y, unsigned char* arg,
+                       void* stream);
+int md2_maxpool3s2_bwd(const float* dy, const unsigned char* arg, int n, int c, int h, int w,
+                       float* dx, void* stream);
+int md2_upsample2_fwd(const float* x, int n, int c, int h, int w, float* y, void* stream);
+int md2_upsample2_bwd(const float* dy, int n, int c, int h, int w, float* dx, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Model: Model(ResidualNetwork(arch), DepthDecoder(embedding_levels=0), PoseDecoder) in mono
  * mode (src/model.jl:24-70), train_loss (src/training.jl:21-78), its pullback, Flux ADAM.
  * Parameters / gradients are CALLER-owned flat fp32 device vectors; their order is the table

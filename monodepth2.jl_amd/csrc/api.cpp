@@ -7,6 +7,7 @@
 #include "conv.h"
 #include "loss_tail.h"
 #include "model.h"
+#include "nn.h"
 
 #include <algorithm>
 
@@ -175,6 +176,26 @@ int md2_act_backward(const float* out, const float* dout, float* dpre, long long
                      void* stream) {
   MD2_CHECK_ARG(out && dout && dpre && n >= 0, "act_backward args");
   return act_backward(out, dout, dpre, (long)n, act, (hipStream_t)stream);
+}
+
+// ---- pooling / resampling --------------------------------------------------------------------
+int md2_maxpool3s2_fwd(const float* x, int n, int c, int h, int w, float* y, unsigned char* arg,
+                       void* stream) {
+  MD2_CHECK_ARG(x && y && arg && n > 0 && c > 0 && h > 0 && w > 0, "maxpool3s2_fwd args");
+  return maxpool_fwd(x, n, c, h, w, y, arg, (h + 1) / 2, (w + 1) / 2, (hipStream_t)stream);
+}
+int md2_maxpool3s2_bwd(const float* dy, const unsigned char* arg, int n, int c, int h, int w,
+                       float* dx, void* stream) {
+  MD2_CHECK_ARG(dy && arg && dx && n > 0 && c > 0 && h > 0 && w > 0, "maxpool3s2_bwd args");
+  return maxpool_bwd(dy, arg, n, c, h, w, (h + 1) / 2, (w + 1) / 2, dx, (hipStream_t)stream);
+}
+int md2_upsample2_fwd(const float* x, int n, int c, int h, int w, float* y, void* stream) {
+  MD2_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0, "upsample2_fwd args");
+  return upsample2_fwd(x, n, c, h, w, y, (hipStream_t)stream);
+}
+int md2_upsample2_bwd(const float* dy, int n, int c, int h, int w, float* dx, void* stream) {
+  MD2_CHECK_ARG(dy && dx && n > 0 && c > 0 && h > 0 && w > 0, "upsample2_bwd args");
+  return upsample2_bwd(dy, n, c, h, w, dx, (hipStream_t)stream);
 }
 
 // ---- model -----------------------------------------------------------------------------------

@@ -61,17 +61,23 @@ size_t conv_dgrad_packed_elems(const ConvShape& s);
 int conv_pack_fwd(const ConvShape& s, const float* w, float* packed, hipStream_t st);
 int conv_pack_dgrad(const ConvShape& s, const float* w, float* packed, hipStream_t st);
 
-// all packs of a model in ONE launch: a device-resident job table (blocks of 256 elements)
-struct PackJob {
-  const float* w;
-  float* out;
-  int mode;            // 0 forward, 1 dgrad
+// all packs of a model in ONE launch: a device-resident job table.  A job is one conv weight
+// read once in source order [Cout][Cin][KK] and scattered into its forward and (optional) dgrad
+// packed layouts; the zero padding of those buffers is written once at allocation
+// (conv_pack_zero), not per update.
+struct PackDst {
+  float* out;          // nullptr: not packed
   int tap;             // tap-major K order (conv_tap_major)
   int layout;          // 0: [Kpad][Mpad]; 1: [Kpad/16][Mpad][16] (k-contiguous chunks, conv_px2)
-  int Cout, Cin, KK, Kpad, Mpad;
+  int Mpad;
+};
+struct PackJob {
+  const float* w;
+  PackDst f, d;        // forward (k over Cin, rows Cout) / dgrad (k over Cout, rows Cin)
+  int Cout, Cin, KK;
   long block_begin;    // first 256-element block of this job in the batched grid
 };
-PackJob conv_pack_job(const ConvShape& s, int mode, const float* w, float* out);
+PackJob conv_pack_job(const ConvShape& s, const float* w, float* out_f, float* out_d);
 long conv_pack_job_blocks(const PackJob& j);
 int conv_pack_batch(const PackJob* dev_jobs, int njobs, long total_blocks, hipStream_t st);
 

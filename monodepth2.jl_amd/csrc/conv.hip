@@ -40,7 +40,20 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // ---------------------------------------------------------------------------------------------
 // forward:  Wt[k][m] = W[m][c][tap]   ([Kpad][Mpad]);   dgrad: Wd[k][ci] = W[co][ci][tap]
 // ([Kdpad][Cinpad]); k = tap*C + c (tap-major) or c*KK + tap, C = Cin (forward) / Cout (dgrad)
-__device__ __forceinline__ float pack_value(const PackJob& j, long idx) {
+struct PackOne {
+  const float* w;
+  float* out;
+  int mode, tap, layout, Cout, Cin, KK, Kpad, Mpad;
+};
+
+__device__ __forceinline__ long packed_index(int k, int m, int layout, int Mpad) {
+  return layout ? ((long)(k >> 4) * Mpad + m) * 16 + (k & 15) : (long)k * Mpad + m;
+}
+
+// single-operand pack (op-level ABI): destination order, writes the zero padding too
+__global__ __launch_bounds__(256) void pack_one_kernel(PackOne j) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)j.Kpad * j.Mpad) return;
   int k, m;
   if (j.layout) {
     const long chunk = (long)j.Mpad * 16;
@@ -54,22 +67,20 @@ __device__ __forceinline__ float pack_value(const PackJob& j, long idx) {
   }
   const int C = j.mode == 0 ? j.Cin : j.Cout;     // reduction channels
   const int Mr = j.mode == 0 ? j.Cout : j.Cin;    // rows
-  if (k >= C * j.KK || m >= Mr) return 0.f;
-  int c, tap;
-  if (j.tap) {
-    tap = k / C;
-    c = k - tap * C;
-  } else {
-    c = k / j.KK;
-    tap = k - c * j.KK;
+  float v = 0.f;
+  if (k < C * j.KK && m < Mr) {
+    int c, tap;
+    if (j.tap) {
+      tap = k / C;
+      c = k - tap * C;
+    } else {
+      c = k / j.KK;
+      tap = k - c * j.KK;
+    }
+    const long co = j.mode == 0 ? m : c, ci = j.mode == 0 ? c : m;
+    v = j.w[(co * j.Cin + ci) * j.KK + tap];
   }
-  const long co = j.mode == 0 ? m : c, ci = j.mode == 0 ? c : m;
-  return j.w[(co * j.Cin + ci) * j.KK + tap];
-}
-
-__global__ __launch_bounds__(256) void pack_one_kernel(PackJob j) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx < (long)j.Kpad * j.Mpad) j.out[idx] = pack_value(j, idx);
+  j.out[idx] = v;
 }
 
 size_t conv_fwd_packed_elems(const ConvShape& s) {
@@ -79,31 +90,19 @@ size_t conv_dgrad_packed_elems(const ConvShape& s) {
   return (size_t)round_up((long)s.Cout * s.KH * s.KW, KPAD) * round_up(s.Cin, MPAD);
 }
 
-PackJob conv_pack_job(const ConvShape& s, int mode, const float* w, float* out) {
-  PackJob j{};
+static int pack_single(const ConvShape& s, int mode, const float* w, float* packed, hipStream_t st) {
+  PackOne j{};
   j.w = w;
-  j.out = out;
+  j.out = packed;
   j.mode = mode;
   j.tap = conv_tap_major(s, mode) ? 1 : 0;
   j.layout = conv_px2_used(s, mode) ? 1 : 0;
   j.Cout = s.Cout;
   j.Cin = s.Cin;
   j.KK = s.KH * s.KW;
-  if (mode == 0) {
-    j.Kpad = (int)round_up((long)s.Cin * j.KK, KPAD);
-    j.Mpad = (int)round_up(s.Cout, MPAD);
-  } else {
-    j.Kpad = (int)round_up((long)s.Cout * j.KK, KPAD);
-    j.Mpad = (int)round_up(s.Cin, MPAD);
-  }
-  return j;
-}
-
-long conv_pack_job_blocks(const PackJob& j) { return cdiv((long)j.Kpad * j.Mpad, 256); }
-
-static int pack_single(const ConvShape& s, int mode, const float* w, float* packed, hipStream_t st) {
-  const PackJob j = conv_pack_job(s, mode, w, packed);
-  hipLaunchKernelGGL(pack_one_kernel, dim3(conv_pack_job_blocks(j)), dim3(256), 0, st, j);
+  j.Kpad = (int)(mode == 0 ? round_up((long)s.Cin * j.KK, KPAD) : round_up((long)s.Cout * j.KK, KPAD));
+  j.Mpad = (int)(mode == 0 ? round_up(s.Cout, MPAD) : round_up(s.Cin, MPAD));
+  hipLaunchKernelGGL(pack_one_kernel, dim3(cdiv((long)j.Kpad * j.Mpad, 256)), dim3(256), 0, st, j);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -114,8 +113,25 @@ int conv_pack_dgrad(const ConvShape& s, const float* w, float* packed, hipStream
   return pack_single(s, 1, w, packed, st);
 }
 
+PackJob conv_pack_job(const ConvShape& s, const float* w, float* out_f, float* out_d) {
+  PackJob j{};
+  j.w = w;
+  j.Cout = s.Cout;
+  j.Cin = s.Cin;
+  j.KK = s.KH * s.KW;
+  j.f = PackDst{out_f, conv_tap_major(s, 0) ? 1 : 0, conv_px2_used(s, 0) ? 1 : 0,
+                (int)round_up(s.Cout, MPAD)};
+  j.d = PackDst{out_d, conv_tap_major(s, 1) ? 1 : 0, conv_px2_used(s, 1) ? 1 : 0,
+                (int)round_up(s.Cin, MPAD)};
+  return j;
+}
+
+long conv_pack_job_blocks(const PackJob& j) { return cdiv((long)j.Cout * j.Cin * j.KK, 256); }
+
+// Source-ordered: consecutive threads read consecutive weights (coalesced, each weight read
+// once); the two scattered writes of a block land in a few packed rows that L2 merges into
+// full lines.  Destination padding is never touched (zeroed at allocation).
 __global__ __launch_bounds__(256) void pack_batch_kernel(const PackJob* __restrict__ jobs, int njobs) {
-  // find the job of this block (jobs sorted by block_begin; few dozen entries)
   __shared__ int s_job;
   if (threadIdx.x == 0) {
     int lo = 0, hi = njobs - 1;
@@ -126,9 +142,23 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const PackJob* __restri
     s_job = lo;
   }
   __syncthreads();
-  const PackJob j = jobs[s_job];
-  const long idx = ((long)blockIdx.x - j.block_begin) * 256 + threadIdx.x;
-  if (idx < (long)j.Kpad * j.Mpad) j.out[idx] = pack_value(j, idx);
+  const PackJob& j = jobs[__builtin_amdgcn_readfirstlane(s_job)];
+  const unsigned e = (unsigned)(blockIdx.x - j.block_begin) * 256u + threadIdx.x;
+  const unsigned KK = (unsigned)j.KK, Cin = (unsigned)j.Cin;
+  if (e >= (unsigned)j.Cout * Cin * KK) return;
+  const float v = j.w[e];
+  const unsigned row = e / KK;
+  const int tap = (int)(e - row * KK);
+  const int co = (int)(row / Cin);
+  const int ci = (int)(row - (unsigned)co * Cin);
+  if (j.f.out) {
+    const int k = j.f.tap ? tap * j.Cin + ci : ci * j.KK + tap;
+    j.f.out[packed_index(k, co, j.f.layout, j.f.Mpad)] = v;
+  }
+  if (j.d.out) {
+    const int k = j.d.tap ? tap * j.Cout + co : co * j.KK + tap;
+    j.d.out[packed_index(k, ci, j.d.layout, j.d.Mpad)] = v;
+  }
 }
 
 int conv_pack_batch(const PackJob* dev_jobs, int njobs, long total_blocks, hipStream_t st) {

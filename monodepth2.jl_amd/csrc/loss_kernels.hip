@@ -522,55 +522,75 @@ __device__ __forceinline__ float up_weight(int X, int j, int in, float r) {
   return (i0 == j ? 1.f - f : 0.f) + (i1 == j ? f : 0.f);
 }
 
+// One block per (low-res row i, sample n).  The mean-normalisation constant is reduced once
+// per block; the row's full-res support rows are contracted column-wise into LDS (coalesced
+// reads of g), then each low-res column contracts its support columns from LDS.
 __global__ __launch_bounds__(256) void up_adjoint_kernel(UpAdjArgs a) {
+  extern __shared__ float s_col[];           // [W]
+  __shared__ float s_red[2][4];
   const int W = a.W, H = a.H;
-  const long total = (long)a.N * a.dw * a.dh;
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= total) return;
-  const int j = (int)(idx % a.dw);
-  const int i = (int)((idx / a.dw) % a.dh);
-  const int n = (int)(idx / ((long)a.dw * a.dh));
+  const int i = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
   float cn = 0.f;
   if (a.smooth_partials) {
     float m = 0.f, T = 0.f;
-    for (int k = 0; k < a.mean_parts; ++k) m += a.mean_partials[n * a.mean_parts + k];
-    for (int k = 0; k < a.smooth_parts; ++k) T += a.smooth_partials[((long)n * a.smooth_parts + k) * 2 + 1];
+    for (int k = tid; k < a.mean_parts; k += 256) m += a.mean_partials[n * a.mean_parts + k];
+    for (int k = tid; k < a.smooth_parts; k += 256)
+      T += a.smooth_partials[((long)n * a.smooth_parts + k) * 2 + 1];
+    m = wave_sum(m);
+    T = wave_sum(T);
+    if ((tid & 63) == 0) {
+      s_red[0][tid >> 6] = m;
+      s_red[1][tid >> 6] = T;
+    }
+    __syncthreads();
+    m = (s_red[0][0] + s_red[0][1]) + (s_red[0][2] + s_red[0][3]);
+    T = (s_red[1][0] + s_red[1][1]) + (s_red[1][2] + s_red[1][3]);
     m = m / ((float)W * (float)H);
     const float mi = 1.f / (m + 1e-7f);
     cn = -a.ws * T * mi * mi / ((float)W * (float)H);
   }
   const float* g = a.g_full + (long)n * W * H;
-  float acc = 0.f;
-  if (a.dw == W && a.dh == H) {
-    acc = g[(long)i * W + j] + cn;
-  } else {
-    int xlo, xhi, ylo, yhi;
-    up_range(j, a.dw, W, a.rx, xlo, xhi);
+  const long orow = ((long)n * a.dh + i) * a.dw;
+  const bool direct = a.dw == W && a.dh == H;
+  float wys = 0.f;
+  if (!direct) {
+    int ylo, yhi;
     up_range(i, a.dh, H, a.ry, ylo, yhi);
-    float wxs = 0.f;
-    for (int X = xlo; X <= xhi; ++X) wxs += up_weight(X, j, a.dw, a.rx);
-    float wys = 0.f;
-    for (int Y = ylo; Y <= yhi; ++Y) {
-      const float wy = up_weight(Y, i, a.dh, a.ry);
-      wys += wy;
-      if (wy == 0.f) continue;
-      float row = 0.f;
+    for (int Y = ylo; Y <= yhi; ++Y) wys += up_weight(Y, i, a.dh, a.ry);
+    for (int X = tid; X < W; X += 256) {
+      float c = 0.f;
+      for (int Y = ylo; Y <= yhi; ++Y) {
+        const float wy = up_weight(Y, i, a.dh, a.ry);
+        if (wy != 0.f) c += wy * g[(long)Y * W + X];
+      }
+      s_col[X] = c;
+    }
+    __syncthreads();
+  }
+  for (int j = tid; j < a.dw; j += 256) {
+    float acc;
+    if (direct) {
+      acc = g[(long)i * W + j] + cn;
+    } else {
+      int xlo, xhi;
+      up_range(j, a.dw, W, a.rx, xlo, xhi);
+      float row = 0.f, wxs = 0.f;
       for (int X = xlo; X <= xhi; ++X) {
         const float wx = up_weight(X, j, a.dw, a.rx);
-        if (wx != 0.f) row += wx * g[(long)Y * W + X];
+        wxs += wx;
+        row += wx * s_col[X];
       }
-      acc += wy * row;
+      acc = row + cn * wxs * wys;
     }
-    acc += cn * wxs * wys;
+    if (a.sigmoid) {
+      const float sg = a.disp[orow + j];
+      acc *= sg * (1.f - sg);
+    }
+    if (a.accumulate)
+      a.out[orow + j] += acc;
+    else
+      a.out[orow + j] = acc;
   }
-  if (a.sigmoid) {
-    const float s = a.disp[idx];
-    acc *= s * (1.f - s);
-  }
-  if (a.accumulate)
-    a.out[idx] += acc;
-  else
-    a.out[idx] = acc;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -797,8 +817,10 @@ int launch_smooth(const SmoothArgs& a, int C, hipStream_t st) {
 }
 
 int launch_up_adjoint(const UpAdjArgs& a, hipStream_t st) {
-  const long total = (long)a.N * a.dw * a.dh;
-  hipLaunchKernelGGL(up_adjoint_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a);
+  const bool direct = a.dw == a.W && a.dh == a.H;
+  const size_t lds = direct ? 0 : (size_t)a.W * sizeof(float);
+  MD2_CHECK_ARG(lds <= 64 * 1024, "up_adjoint: full-res width exceeds the LDS row");
+  hipLaunchKernelGGL(up_adjoint_kernel, dim3(a.dh, a.N), dim3(256), lds, st, a);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }

@@ -282,8 +282,13 @@ class Model {
     r.s.reflect = p.reflect;
     r.s.Ho = out_dim(H, p.k, p.stride, p.pad);
     r.s.Wo = out_dim(W, p.k, p.stride, p.pad);
+    // packed weights: the repack writes only real elements, the padding stays zero from here
     MD2_TRY(alloc(&r.wpf, conv_fwd_packed_elems(r.s)));
-    if (dgrad) MD2_TRY(alloc(&r.wpd, conv_dgrad_packed_elems(r.s)));
+    MD2_HIP(hipMemset(r.wpf, 0, conv_fwd_packed_elems(r.s) * sizeof(float)));
+    if (dgrad) {
+      MD2_TRY(alloc(&r.wpd, conv_dgrad_packed_elems(r.s)));
+      MD2_HIP(hipMemset(r.wpd, 0, conv_dgrad_packed_elems(r.s) * sizeof(float)));
+    }
     return MD2_OK;
   }
   void need_ws(const RConv& r, int nimg, size_t& ws_need, bool dgrad) {
@@ -557,17 +562,15 @@ class Model {
     return t;
   }
 
-  // one batched launch re-packs every conv weight (forward and dgrad layouts) after an update
+  // one batched launch re-packs every conv weight (forward and dgrad layouts) after an update;
+  // each weight is read once and written to both layouts
   PackJob* pack_jobs = nullptr;
   int pack_njobs = 0;
   long pack_blocks = 0;
 
   int build_pack_table() {
     std::vector<PackJob> jobs;
-    auto pk = [&](RConv& c) {
-      jobs.push_back(conv_pack_job(c.s, 0, params + c.p.w, c.wpf));
-      if (c.wpd) jobs.push_back(conv_pack_job(c.s, 1, params + c.p.w, c.wpd));
-    };
+    auto pk = [&](RConv& c) { jobs.push_back(conv_pack_job(c.s, params + c.p.w, c.wpf, c.wpd)); };
     pk(stem);
     for (auto& sg : stages)
       for (auto& b : sg) {

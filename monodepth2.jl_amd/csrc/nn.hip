@@ -319,6 +319,8 @@ int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const
 // ---------------------------------------------------------------------------------------------
 // MaxPool 3x3 / stride 2 / pad 1 (ResNet stem); argmax kept as the window index 0..8
 // ---------------------------------------------------------------------------------------------
+// one output per thread; with an even input width the window columns 2ow, 2ow+1 are one float2
+template <bool EVENW>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restrict__ x, int H, int W,
                                                           float* __restrict__ y,
                                                           unsigned char* __restrict__ arg, int Ho,
@@ -327,72 +329,101 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restric
   if (i >= n) return;
   const uint32_t r = fdiv(i, fdWo), plane = fdiv(r, fdHo);
   const int ow = (int)(i - r * fdWo.d), oh = (int)(r - plane * fdHo.d);
-  const float* p = x + (long)plane * H * W;
+  const float* p = x + plane * (uint32_t)(H * W);
   float best = -INFINITY;
   int bi = 0;
+  const int iw = ow * 2;
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh) {
     const int ih = oh * 2 - 1 + kh;
     if (ih < 0 || ih >= H) continue;
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int iw = ow * 2 - 1 + kw;
-      if (iw < 0 || iw >= W) continue;
-      const float v = p[ih * W + iw];
-      if (v > best) {
-        best = v;
-        bi = kh * 3 + kw;
-      }
+    const float* row = p + ih * W;
+    float v0 = -INFINITY, v1, v2 = -INFINITY;
+    if (iw > 0) v0 = row[iw - 1];
+    if (EVENW) {
+      const float2 t = *reinterpret_cast<const float2*>(row + iw);
+      v1 = t.x;
+      v2 = t.y;
+    } else {
+      v1 = row[iw];
+      if (iw + 1 < W) v2 = row[iw + 1];
     }
+    // strict '>' in (kh, kw) scan order: the first maximum wins (NNlib maxpool)
+    if (v0 > best) { best = v0; bi = kh * 3; }
+    if (v1 > best) { best = v1; bi = kh * 3 + 1; }
+    if (v2 > best) { best = v2; bi = kh * 3 + 2; }
   }
   y[i] = best;
   arg[i] = (unsigned char)bi;
 }
 
-// gather: input (ih, iw) is tap kh = ih + 1 - 2 oh of at most two output rows (same for columns)
+// Gather over 2x2 input blocks: input rows {2i, 2i+1} x columns {2j, 2j+1} are touched only by
+// outputs (i..i+1, j..j+1) -- even rows/columns are tap 1 of output i, odd ones tap 2 of output
+// i and tap 0 of output i+1 -- so each thread reads 4 (arg, dy) pairs and writes 4 inputs.
+template <bool EVENW>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ dy,
                                                           const unsigned char* __restrict__ arg,
-                                                          int H, int Ho, int Wo, FastDiv fdW,
-                                                          FastDiv fdH, float* __restrict__ dx,
+                                                          int H, int W, int Ho, FastDiv fdWo,
+                                                          FastDiv fdHo, float* __restrict__ dx,
                                                           uint32_t n) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t r = fdiv(i, fdW), plane = fdiv(r, fdH);
-  const int iw = (int)(i - r * fdW.d), ih = (int)(r - plane * fdH.d);
-  const long ob = (long)plane * Ho * Wo;
-  const int oh1 = (ih + 1) >> 1, ow1 = (iw + 1) >> 1;     // tap 0/1; oh1-1 has tap 2/3
-  float s = 0.f;
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    const int oh = oh1 - a, kh = ih + 1 - 2 * oh;
-    if (oh < 0 || oh >= Ho || kh > 2) continue;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int ow = ow1 - b, kw = iw + 1 - 2 * ow;
-      if (ow < 0 || ow >= Wo || kw > 2) continue;
-      const long o = ob + oh * Wo + ow;
-      if (arg[o] == kh * 3 + kw) s += dy[o];
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t r = fdiv(t, fdWo), plane = fdiv(r, fdHo);
+  const int Wo = (int)fdWo.d;
+  const int j = (int)(t - r * fdWo.d), i = (int)(r - plane * fdHo.d);
+  const bool hasr = i + 1 < Ho, hasc = j + 1 < Wo;
+  const uint32_t o = t;
+  const int a00 = arg[o];
+  const float g00 = dy[o];
+  int a01 = -1, a10 = -1, a11 = -1;
+  float g01 = 0.f, g10 = 0.f, g11 = 0.f;
+  if (hasc) { a01 = arg[o + 1]; g01 = dy[o + 1]; }
+  if (hasr) { a10 = arg[o + Wo]; g10 = dy[o + Wo]; }
+  if (hasr && hasc) { a11 = arg[o + Wo + 1]; g11 = dy[o + Wo + 1]; }
+  const float e00 = a00 == 4 ? g00 : 0.f;
+  const float e01 = (a00 == 5 ? g00 : 0.f) + (a01 == 3 ? g01 : 0.f);
+  const float e10 = (a00 == 7 ? g00 : 0.f) + (a10 == 1 ? g10 : 0.f);
+  const float e11 = (a00 == 8 ? g00 : 0.f) + (a01 == 6 ? g01 : 0.f) + (a10 == 2 ? g10 : 0.f) +
+                    (a11 == 0 ? g11 : 0.f);
+  float* q = dx + plane * (uint32_t)(H * W) + (2 * i) * W + 2 * j;
+  if (EVENW) {
+    *reinterpret_cast<float2*>(q) = make_float2(e00, e01);
+    if (2 * i + 1 < H) *reinterpret_cast<float2*>(q + W) = make_float2(e10, e11);
+  } else {
+    q[0] = e00;
+    if (2 * j + 1 < W) q[1] = e01;
+    if (2 * i + 1 < H) {
+      q[W] = e10;
+      if (2 * j + 1 < W) q[W + 1] = e11;
     }
   }
-  dx[i] = s;
 }
 
 int maxpool_fwd(const float* x, int N, int C, int H, int W, float* y, unsigned char* arg, int Ho,
                 int Wo, hipStream_t st) {
   const long n = (long)N * C * Ho * Wo;
   MD2_TRY(check_u31((long)N * C * H * W));
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, x, H, W, y, arg, Ho,
-                     fd(Wo), fd(Ho), (uint32_t)n);
+  if (W % 2 == 0)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(cdiv(n, 256)), dim3(256), 0, st, x, H, W, y,
+                       arg, Ho, fd(Wo), fd(Ho), (uint32_t)n);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st, x, H, W, y,
+                       arg, Ho, fd(Wo), fd(Ho), (uint32_t)n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
 
 int maxpool_bwd(const float* dy, const unsigned char* arg, int N, int C, int H, int W, int Ho,
                 int Wo, float* dx, hipStream_t st) {
-  const long n = (long)N * C * H * W;
-  MD2_TRY(check_u31(n));
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, arg, H, Ho, Wo,
-                     fd(W), fd(H), dx, (uint32_t)n);
+  MD2_CHECK_ARG(Ho == (H + 1) / 2 && Wo == (W + 1) / 2, "maxpool_bwd: 3x3/2 pad-1 output shape");
+  const long n = (long)N * C * Ho * Wo;
+  MD2_TRY(check_u31((long)N * C * H * W));
+  if (W % 2 == 0)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, arg, H,
+                       W, Ho, fd(Wo), fd(Ho), dx, (uint32_t)n);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, arg, H,
+                       W, Ho, fd(Wo), fd(Ho), dx, (uint32_t)n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -424,14 +455,27 @@ __global__ __launch_bounds__(256) void upsample2_fwd_kernel(const float* __restr
          fy * ((1.f - fx) * p[y1 * w + x0] + fx * p[y1 * w + x1]);
 }
 
-__device__ __forceinline__ float up_w(int o, int j, float r, int in) {
-  int i0, i1;
-  float f;
-  src_idx(o, r, in, i0, i1, f);
-  return (i0 == j ? 1.f - f : 0.f) + (i1 == j ? f : 0.f);
+// Adjoint as a gather.  For the x2 align-corners map s = r*o, r = (n-1)/(2n-1), 1/r = 2+1/(n-1):
+// input i receives from outputs with floor(s) in {i-1, i}, i.e. o in [2i-2, 2i+3] (r*o is never
+// within float rounding of an integer except at the end points, which stay inside the range).
+// The six per-axis weights are computed once, with the forward's exact float arithmetic.
+__device__ __forceinline__ void up_adj_weights(int i, float r, int in, int out, int& o0,
+                                               float wv[6]) {
+  o0 = 2 * i - 2;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int o = o0 + q;
+    float wq = 0.f;
+    if (o >= 0 && o < out) {
+      int i0, i1;
+      float f;
+      src_idx(o, r, in, i0, i1, f);
+      wq = (i0 == i ? 1.f - f : 0.f) + (i1 == i ? f : 0.f);
+    }
+    wv[q] = wq;
+  }
 }
 
-// gather adjoint: input pixel (iy, ix) collects the output pixels whose 2x2 stencil touches it
 __global__ __launch_bounds__(256) void upsample2_bwd_kernel(const float* __restrict__ dy, int h,
                                                             int w, float ry, float rx, FastDiv fdw,
                                                             FastDiv fdh, float* __restrict__ dx,
@@ -441,22 +485,21 @@ __global__ __launch_bounds__(256) void upsample2_bwd_kernel(const float* __restr
   const int W2 = 2 * w, H2 = 2 * h;
   const uint32_t r = fdiv(i, fdw), plane = fdiv(r, fdh);
   const int ix = (int)(i - r * fdw.d), iy = (int)(r - plane * fdh.d);
-  const float* g = dy + (long)plane * H2 * W2;
-  // outputs o with floor(o*r) in {i-1, i}:  o in [(i-1)/r, (i+1)/r]
-  const int ylo = (h == 1) ? 0 : max(0, (int)floorf((float)(iy - 1) / ry) - 1);
-  const int yhi = (h == 1) ? H2 - 1 : min(H2 - 1, (int)ceilf((float)(iy + 1) / ry) + 1);
-  const int xlo = (w == 1) ? 0 : max(0, (int)floorf((float)(ix - 1) / rx) - 1);
-  const int xhi = (w == 1) ? W2 - 1 : min(W2 - 1, (int)ceilf((float)(ix + 1) / rx) + 1);
+  const float* g = dy + plane * (uint32_t)(H2 * W2);
+  int oy0, ox0;
+  float wy[6], wx[6];
+  up_adj_weights(iy, ry, h, H2, oy0, wy);
+  up_adj_weights(ix, rx, w, W2, ox0, wx);
   float s = 0.f;
-  for (int oy = ylo; oy <= yhi; ++oy) {
-    const float wy = up_w(oy, iy, ry, h);
-    if (wy == 0.f) continue;
-    float row = 0.f;
-    for (int ox = xlo; ox <= xhi; ++ox) {
-      const float wx = up_w(ox, ix, rx, w);
-      if (wx != 0.f) row += wx * g[oy * W2 + ox];
-    }
-    s += wy * row;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    if (wy[a] == 0.f) continue;
+    const float* row = g + (oy0 + a) * W2;
+    float acc = 0.f;
+#pragma unroll
+    for (int b = 0; b < 6; ++b)
+      if (wx[b] != 0.f) acc += wx[b] * row[ox0 + b];
+    s += wy[a] * acc;
   }
   dx[i] = s;
 }

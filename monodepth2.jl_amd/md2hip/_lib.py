@@ -77,6 +77,10 @@ _SIGS = {
     "md2_conv2d_dgrad": (C.c_int, [C.POINTER(ConvDesc), P, P, P, P, P]),
     "md2_conv2d_wgrad": (C.c_int, [C.POINTER(ConvDesc), P, P, P, P, P, P]),
     "md2_act_backward": (C.c_int, [P, P, P, C.c_longlong, C.c_int, P]),
+    "md2_maxpool3s2_fwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
+    "md2_maxpool3s2_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "md2_upsample2_fwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "md2_upsample2_bwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "md2_arch_param_count": (C.c_int, [C.POINTER(ModelCfg), C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     "md2_arch_param_info": (C.c_int, [C.POINTER(ModelCfg), C.c_int, C.c_char_p, C.c_int,
                                       C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_longlong)]),

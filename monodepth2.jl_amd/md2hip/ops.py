@@ -70,3 +70,43 @@ def act_backward(out, dout, act):
     check(lib().md2_act_backward(ptr(out), ptr(dout), ptr(dpre), dout.numel(), ACT[act],
                                  stream_of(out.device)), "md2_act_backward")
     return dpre
+
+
+def maxpool3s2(x):
+    """ResNet stem ``MaxPool((3,3), pad=1, stride=2)``: (y, arg) with arg the uint8 window index
+    of the first maximum, kept for :func:`maxpool3s2_backward`."""
+    import torch
+    n, c, h, w = x.shape
+    y = torch.empty(n, c, (h + 1) // 2, (w + 1) // 2, dtype=torch.float32, device=x.device)
+    arg = torch.empty(y.shape, dtype=torch.uint8, device=x.device)
+    check(lib().md2_maxpool3s2_fwd(ptr(x), n, c, h, w, ptr(y), ptr(arg), stream_of(x.device)),
+          "md2_maxpool3s2_fwd")
+    return y, arg
+
+
+def maxpool3s2_backward(dy, arg, x_shape):
+    import torch
+    n, c, h, w = x_shape
+    dx = torch.empty(n, c, h, w, dtype=torch.float32, device=dy.device)
+    check(lib().md2_maxpool3s2_bwd(ptr(dy), ptr(arg), n, c, h, w, ptr(dx), stream_of(dy.device)),
+          "md2_maxpool3s2_bwd")
+    return dx
+
+
+def upsample2(x):
+    """``upsample_bilinear(x, (2,2))`` with align_corners (src/depth_decoder.jl:18-19)."""
+    import torch
+    n, c, h, w = x.shape
+    y = torch.empty(n, c, 2 * h, 2 * w, dtype=torch.float32, device=x.device)
+    check(lib().md2_upsample2_fwd(ptr(x), n, c, h, w, ptr(y), stream_of(x.device)),
+          "md2_upsample2_fwd")
+    return y
+
+
+def upsample2_backward(dy):
+    import torch
+    n, c, h2, w2 = dy.shape
+    dx = torch.empty(n, c, h2 // 2, w2 // 2, dtype=torch.float32, device=dy.device)
+    check(lib().md2_upsample2_bwd(ptr(dy), n, c, h2 // 2, w2 // 2, ptr(dx), stream_of(dy.device)),
+          "md2_upsample2_bwd")
+    return dx
