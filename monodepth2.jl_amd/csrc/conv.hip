@@ -14,6 +14,7 @@
 // the 64-cycle f32 MFMAs.  Small-M / huge-K shapes (layer4, wgrad) use split-K slabs reduced by
 // a second kernel that also applies the epilogue (deterministic, no atomics).
 #include "conv.h"
+#include "head.h"
 
 namespace md2 {
 
@@ -899,6 +900,30 @@ bool conv_tap_major(const ConvShape& s, int mode) {
   }
 }
 
+// Cout = 1 3x3 convs (disparity heads) run the VALU kernels of head.hip; MD2_HEAD=0 disables
+static bool head_path(const ConvShape& s) {
+  static const int on = [] {
+    const char* e = getenv("MD2_HEAD");
+    return e ? atoi(e) : 1;
+  }();
+  return on && head_conv_ok(s);
+}
+// tap (c, t) of the packed operand: forward rows m = 0, k = t*Cin + c or c*9 + t; dgrad
+// k = co*9 + t = t (Cout = 1, channel-major), row c
+static HeadW head_w(const ConvShape& s, int mode, const float* packed) {
+  HeadW w{packed, 0, 0};
+  if (mode == 0) {
+    const long Mpad = round_up(s.Cout, MPAD);
+    if (conv_tap_major(s, 0)) { w.sc = Mpad; w.st = (long)s.Cin * Mpad; }
+    else { w.sc = 9 * Mpad; w.st = Mpad; }
+  } else {
+    w.sc = 1;
+    w.st = round_up(s.Cin, MPAD);
+  }
+  return w;
+}
+static HeadIn head_in(const TensorIn& x) { return HeadIn{x.p0, x.bs0, x.bdiv, x.bhi}; }
+
 size_t conv_fwd_workspace(const ConvShape& s) {
   const long N = (long)s.N * s.Ho * s.Wo;
   const Plan p = plan_px(s.Cout, N, s.Cin * s.KH * s.KW);   // BK does not change the split count
@@ -933,6 +958,7 @@ static size_t wgrad_ws_bytes(const ConvShape& s, int c0) {
 
 // the split count depends on the concat split only through CW: size for every possible CW
 size_t conv_wgrad_workspace(const ConvShape& s) {
+  if (head_path(s)) return head_wgrad_workspace(s);
   size_t b = wgrad_ws_bytes(s, s.Cin);
   for (int c0 = 16; c0 <= 128; c0 *= 2) b = std::max(b, wgrad_ws_bytes(s, c0));
   return b;
@@ -945,6 +971,11 @@ int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const 
   MD2_CHECK_ARG(x.c0 == s.Cin || x.p1 != nullptr, "conv_fwd: second input tensor missing");
   MD2_CHECK_ARG(x.c0 >= s.Cin || !conv_tap_major(s, 0) || x.c0 % 16 == 0,
                 "conv_fwd: concat split must be a multiple of 16 channels");
+  if (head_path(s) && x.c0 >= s.Cin && y.c0 >= 1) {
+    MD2_CHECK_ARG(!conv_px2_used(s, 0), "head: packed layout");
+    return head_fwd(s, head_in(x), head_w(s, 0, wpacked), y.bias, y.act, y.p0, y.bs0,
+                    y.accumulate, st);
+  }
   ConvArgs a{};
   fill_common(a, s);
   a.g.M = s.Cout;
@@ -978,6 +1009,10 @@ int conv_dgrad(const ConvShape& s, const float* dy, const float* wpacked_d, cons
   MD2_TRY(check_shape(s));
   MD2_CHECK_ARG(dy && wpacked_d && dx.p0, "conv_dgrad pointers");
   MD2_CHECK_ARG(!dx.bias && dx.act == ACT_NONE, "conv_dgrad: no bias/activation on dX");
+  if (head_path(s) && dx.c0 >= s.Cin) {
+    MD2_CHECK_ARG(!conv_px2_used(s, 1) && !conv_tap_major(s, 1), "head: packed layout");
+    return head_dgrad(s, dy, head_w(s, 1, wpacked_d), dx.p0, dx.bs0, dx.accumulate, st);
+  }
   ConvArgs a{};
   fill_common(a, s);
   a.g.M = s.Cin;
@@ -1021,6 +1056,8 @@ int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw
   MD2_TRY(check_shape(s));
   MD2_CHECK_ARG(x.p0 && dy && dw, "conv_wgrad pointers");
   MD2_CHECK_ARG(x.c0 >= s.Cin || x.p1 != nullptr, "conv_wgrad: second input tensor missing");
+  if (head_path(s) && x.c0 >= s.Cin)
+    return head_wgrad(s, head_in(x), dy, dw, db, accumulate, ws.ptr, ws.bytes, st);
   const WPlan p = plan_wgrad(s, x.c0);
   const bool tap = p.cw > 0;
   ConvArgs a{};

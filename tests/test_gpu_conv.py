@@ -44,6 +44,15 @@ CASES = [
     ((6, 256, 4, 8), 512, 1, 2, 0, False, None, False),          # layer4 downsample
     ((2, 512, 2, 4), 256, 3, 1, 1, True, "elu", True),           # branch1.c1 reflect 2x4
     ((4, 512, 2, 4), 256, 3, 1, 1, False, "relu", True),         # pose conv1 on 2x4
+    # Cout = 1 heads (VALU kernels of head.hip): reflect folds on 2/3-wide maps, zero padding,
+    # ragged and > 8-channel groups, the bench-size full-resolution head
+    ((2, 16, 2, 2), 1, 3, 1, 1, True, "sigmoid", True),          # every pixel folds twice
+    ((2, 8, 3, 3), 1, 3, 1, 1, True, "sigmoid", True),           # q = 1 = n-2 folds both ways
+    ((3, 5, 7, 11), 1, 3, 1, 1, True, "sigmoid", True),          # ragged channel group
+    ((2, 13, 6, 9), 1, 3, 1, 1, False, None, True),              # zero padding, no act
+    ((2, 32, 16, 52), 1, 3, 1, 1, True, "sigmoid", True),        # head4 geometry
+    ((2, 128, 4, 13), 1, 3, 1, 1, True, "sigmoid", True),        # head2 (16 channel groups)
+    ((12, 16, 128, 416), 1, 3, 1, 1, True, "sigmoid", True),     # head5 at bench size
 ]
 
 
