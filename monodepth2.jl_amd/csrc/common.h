@@ -92,12 +92,53 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 // Deterministic block sum of NV values per thread (blockDim.x == 256).  Result valid in
+// ---- raw buffer loads: scalar resource + 32-bit per-lane byte offset (+ wave-uniform soffset)
+constexpr uint32_t OOB = 0x7ffffff0u;   // byte offset that is out of range for every tensor
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off_bytes, 0, 0));
+}
+// voffset (per lane; OOB for padding) + soffset (wave-uniform channel step); OOB + soffset stays
+// below 2^32 and beyond every extent, whether or not the range check includes soffset
+__device__ __forceinline__ float bload_s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, 0);
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                     __uint_as_float(v[3]));
+}
+
+// Wave sum by DPP (no LDS traffic): quad permutes and row shifts form the 16-lane row sums,
+// row_bcast:15 / row_bcast:31 fold the four rows into lane 63, which is broadcast.
+__device__ __forceinline__ float dpp_add(float v, int ctrl_sel) {
+  int r;
+  const int x = __builtin_bit_cast(int, v);
+  switch (ctrl_sel) {
+    case 0: r = __builtin_amdgcn_update_dpp(0, x, 0xb1, 0xf, 0xf, true); break;    // quad 1,0,3,2
+    case 1: r = __builtin_amdgcn_update_dpp(0, x, 0x4e, 0xf, 0xf, true); break;    // quad 2,3,0,1
+    case 2: r = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true); break;   // row_shr:4
+    case 3: r = __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true); break;   // row_shr:8
+    case 4: r = __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false); break;  // row_bcast:15
+    default: r = __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false); break; // row_bcast:31
+  }
+  return v + __builtin_bit_cast(float, r);
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+#pragma unroll
+  for (int k = 0; k < 6; ++k) v = dpp_add(v, k);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
 // threadIdx.x == 0 only.  `red` must hold 4*NV floats of LDS.
 template <int NV>
 __device__ __forceinline__ void block_sum256(float (&v)[NV], float* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum_dpp(v[i]);
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) red[wid * NV + i] = v[i];

@@ -219,25 +219,6 @@ __device__ __forceinline__ void out_pixel(const ConvArgs& a, bool phase, long nn
   }
 }
 
-constexpr uint32_t OOB = 0x7ffffff0u;   // byte offset that is out of range for every tensor
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off_bytes, 0, 0));
-}
-// voffset (per lane; OOB for padding) + soffset (wave-uniform channel step); OOB + soffset stays
-// below 2^32 and beyond every extent, whether or not the range check includes soffset
-__device__ __forceinline__ float bload_s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
-}
-__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, 0);
-  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
-                     __uint_as_float(v[3]));
-}
-
 template <int TM, int TN, int BK>
 __device__ __forceinline__ void mma_chunk(const float* __restrict__ As, int lda,
                                           const float* __restrict__ Bs, int ldb, int am0, int bn0,
