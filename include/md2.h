@@ -174,6 +174,12 @@ int md2_model_forward_loss(md2_model* m, const float* x, const float* auto_loss,
 int md2_model_num_segments(md2_model* m);
 int md2_model_backward_segment(md2_model* m, int k, long long* off, long long* len,
                                void* stream);
+/* update!(ADAM(lr, (beta1, beta2)), θ, ∇) on any flat fp32 device vector of n elements (Flux
+ * ADAM, eps on the bias-corrected sqrt(v)); `step` >= 1 counts updates of this vector; the
+ * gradient is scaled by grad_scale first (1/world for a summed DP gradient).  The free-variable
+ * loop of slow_depth (src/simple_depth.jl:20-43) uses it directly. */
+int md2_adam(float* p, const float* g, float* adam_m, float* adam_v, long long n, float lr,
+             float beta1, float beta2, float eps, int step, float grad_scale, void* stream);
 /* Flux ADAM step over the flat vectors (bias correction with `step` >= 1); gradients are
  * multiplied by grad_scale first (1/world_size after a sum all-reduce); re-packs weights */
 int md2_model_adam(md2_model* m, float* adam_m, float* adam_v, float lr, float beta1,

@@ -1,6 +1,7 @@
 // C ABI of libmd2hip.so (include/md2.h).
 #include "../../include/md2.h"
 
+#include <cmath>
 #include <cstring>
 #include <string>
 
@@ -176,6 +177,15 @@ int md2_act_backward(const float* out, const float* dout, float* dpre, long long
                      void* stream) {
   MD2_CHECK_ARG(out && dout && dpre && n >= 0, "act_backward args");
   return act_backward(out, dout, dpre, (long)n, act, (hipStream_t)stream);
+}
+
+// ---- optimiser ---------------------------------------------------------------------------------
+int md2_adam(float* p, const float* g, float* adam_m, float* adam_v, long long n, float lr,
+             float beta1, float beta2, float eps, int step, float grad_scale, void* stream) {
+  MD2_CHECK_ARG(p && g && adam_m && adam_v && n > 0 && step >= 1, "adam args");
+  const double bc1 = 1.0 - std::pow((double)beta1, step), bc2 = 1.0 - std::pow((double)beta2, step);
+  return adam_step(p, g, adam_m, adam_v, (long)n, lr, beta1, beta2, eps, (float)bc1, (float)bc2,
+                   grad_scale, (hipStream_t)stream);
 }
 
 // ---- pooling / resampling --------------------------------------------------------------------

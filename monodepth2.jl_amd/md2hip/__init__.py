@@ -8,7 +8,9 @@ from ._lib import MD2Error, lib  # noqa: F401
 from .loss import Params, TrainCache, depth10k_intrinsics, loss_tail, pack_poses  # noqa: F401
 from .model import (ADAM, DepthDecoder, Model, Pose, PoseDecoder, ResidualNetwork, ResNet,  # noqa: F401
                     eval_disparity, gradient, param_table, train_loss, train_step)
+from .slow_depth import SlowDepth, adam_update, slow_depth  # noqa: F401
 
 __all__ = ["Params", "TrainCache", "depth10k_intrinsics", "loss_tail", "pack_poses", "lib", "MD2Error",
            "ADAM", "DepthDecoder", "Model", "Pose", "PoseDecoder", "ResidualNetwork", "ResNet",
-           "eval_disparity", "gradient", "param_table", "train_loss", "train_step"]
+           "eval_disparity", "gradient", "param_table", "train_loss", "train_step",
+           "SlowDepth", "adam_update", "slow_depth"]

@@ -77,6 +77,8 @@ _SIGS = {
     "md2_conv2d_dgrad": (C.c_int, [C.POINTER(ConvDesc), P, P, P, P, P]),
     "md2_conv2d_wgrad": (C.c_int, [C.POINTER(ConvDesc), P, P, P, P, P, P]),
     "md2_act_backward": (C.c_int, [P, P, P, C.c_longlong, C.c_int, P]),
+    "md2_adam": (C.c_int, [P, P, P, P, C.c_longlong, C.c_float, C.c_float, C.c_float, C.c_float,
+                            C.c_int, C.c_float, P]),
     "md2_maxpool3s2_fwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
     "md2_maxpool3s2_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "md2_upsample2_fwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),

@@ -460,8 +460,8 @@ def resnet_stages(P, x, arch=18):
             stride = 2 if (bi == 0 and si > 0) else 1
             p = f"encoder.layer{si + 1}.{bi}"
             if bottleneck:
-                h = F.relu(batchnorm_train(F.conv2d(y, P[p + ".conv1.weight"]), P[p + ".bn1.gamma"], P[p + ".bn1.beta"]))
-                h = F.relu(batchnorm_train(F.conv2d(h, P[p + ".conv2.weight"], stride=stride, padding=1), P[p + ".bn2.gamma"], P[p + ".bn2.beta"]))
+                h = _relu(batchnorm_train(F.conv2d(y, P[p + ".conv1.weight"]), P[p + ".bn1.gamma"], P[p + ".bn1.beta"]), p + ".relu1")
+                h = _relu(batchnorm_train(F.conv2d(h, P[p + ".conv2.weight"], stride=stride, padding=1), P[p + ".bn2.gamma"], P[p + ".bn2.beta"]), p + ".relu2")
                 h = batchnorm_train(F.conv2d(h, P[p + ".conv3.weight"]), P[p + ".bn3.gamma"], P[p + ".bn3.beta"])
             else:
                 h = _relu(batchnorm_train(F.conv2d(y, P[p + ".conv1.weight"], stride=stride, padding=1), P[p + ".bn1.gamma"], P[p + ".bn1.beta"]), p + ".relu1")
@@ -589,13 +589,18 @@ class Adam:
 
 
 def slow_depth_loss(disp, rvecs, tvecs, x, K, invK, source_ids=(1, 3), target_id=2,
-                    min_depth=0.1, max_depth=100.0):
+                    min_depth=0.1, max_depth=100.0, forced_sel=None, per_source=None):
     """Loss inside the ``gradient(theta)`` closure of ``slow_depth`` (src/simple_depth.jl:25-41):
-    mean(prediction_loss) + smooth_loss(disp) (no 1e-3 weight, no mean normalisation)."""
+    mean(prediction_loss) + smooth_loss(disp) (no 1e-3 weight, no mean normalisation).
+    ``forced_sel`` / ``per_source``: the test hooks of ``loss_from_outputs``."""
     Ps = [composeT(r, t, sid < target_id) for r, t, sid in zip(rvecs, tvecs, source_ids)]
     warped = warp(disp, x, Ps, K, invK, source_ids, min_depth, max_depth)
     target_x = x[:, target_id - 1]
-    return torch.mean(prediction_loss(warped, target_x)) + smooth_loss(disp[:, 0], target_x)
+    src_losses = [photometric_loss(p, target_x) for p in warped]
+    if per_source is not None:
+        per_source.append([l.detach() for l in src_losses])
+    pred = _forced_min(src_losses, forced_sel) if forced_sel is not None else _first_argmin(src_losses)
+    return torch.mean(pred) + smooth_loss(disp[:, 0], target_x)
 
 
 def slow_depth_init(width, height, dtype=torch.float64):

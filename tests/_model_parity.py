@@ -66,8 +66,9 @@ def gpu_decisions(model, N, arch=18, L=3):
         for bi in range(nb):
             q = f"layer{si + 1}.{bi}"
             d[f"encoder.{q}.out"] = nmajor(t[q + ".out"] > 0)
-            if q + ".relu1" in t:
-                d[f"encoder.{q}.relu1"] = nmajor(t[q + ".relu1"] > 0)
+            for r in ("relu1", "relu2"):           # BasicBlock: relu1; Bottleneck: relu1, relu2
+                if f"{q}.{r}" in t:
+                    d[f"encoder.{q}.{r}"] = nmajor(t[f"{q}.{r}"] > 0)
     sq = t["pose.sq"] > 0
     for j in range(2):                       # pair j = frames (j, j+1), GPU pairs [jN, (j+1)N)
         d[f"pose{j}.sqa"] = sq[j * N:(j + 1) * N]
@@ -79,16 +80,19 @@ def gpu_decisions(model, N, arch=18, L=3):
 
 def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=None, sel=None,
                       decisions=None):
-    """Per-tensor gradient error of the SAME oracle run in fp32 vs fp64 (the fp32 noise floor)."""
+    """Per-tensor gradient error of the SAME oracle run in fp32 vs fp64 (the fp32 noise floor),
+    plus the forward outputs' floors under the keys "__disp<s>" and "__pose"."""
     x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
     K, invK = D.intrinsics(W, H)
     spec = O.param_spec(arch, C, (2, 3, 4, 5))
-    grads = []
+    grads, fwd = [], []
     for dt in (torch.float64, torch.float32):
         f = flat.to(dt).clone().requires_grad_(True)
         P = O.unflatten(f, spec)
         with O.forced_decisions(decisions or {}):
             d_o, p_o = O.model_forward(P, x.to(dt), arch=arch)
+        fwd.append(([d.detach().double() for d in d_o],
+                    torch.cat([torch.cat([r, t], 1) for r, t in p_o], 0).detach().double()))
         cache_o = O.TrainCache(K=K.to(dt), invK=invK.to(dt))
         par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
         forced = [s.unsqueeze(1).long() for s in sel]
@@ -101,4 +105,8 @@ def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=
             n *= s
         errs[name] = D.rel_err(grads[1][off:off + n], grads[0][off:off + n])
         off += n
+    # forward outputs: "__disp<s>" per scale and "__pose"
+    for s_, (a, b) in enumerate(zip(fwd[1][0], fwd[0][0])):
+        errs[f"__disp{s_}"] = D.rel_err(a, b)
+    errs["__pose"] = D.rel_err(fwd[1][1], fwd[0][1])
     return errs

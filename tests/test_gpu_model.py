@@ -17,26 +17,30 @@ from tests import _data as D
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("strict", [True, False], ids=["ramp-sources", "texture"])
-def test_model_train_loss_parity(strict):
+@pytest.mark.parametrize("arch,strict", [(18, True), (18, False), (34, True), (50, True)],
+                         ids=["r18-ramp-sources", "r18-texture", "r34-ramp-sources", "r50-ramp-sources"])
+def test_model_train_loss_parity(arch, strict):
+    """ResNet-18 (the measured config), ResNet-34 and the Bottleneck ResNet-50 of config 5."""
     from tests._model_parity import oracle_fp32_floor, run
-    g, o, errs = run(strict=strict)
+    g, o, errs = run(strict=strict, arch=arch)
     assert abs(g["loss"] - o["loss"]) <= 1e-6 * abs(o["loss"])
     assert g["loss"] == g["tail_loss"]
-    for a, b in zip(g["disps"], o["disps"]):
-        assert D.rel_err(a, b) < 1e-5
-    assert D.rel_err(g["pose"], o["pose"]) < 1e-5
-    floor = oracle_fp32_floor(strict=strict, flat=_flat(), sel=[s for s in g["sel"]],
+    floor = oracle_fp32_floor(strict=strict, arch=arch, flat=_flat(arch), sel=[s for s in g["sel"]],
                               decisions=g["decisions"])
+    # forward: 1e-5, or 4x the fp32 floor where deeper encoders round more (ResNet-50's pose
+    # head: the fp32 oracle itself is 3.6e-5 from fp64)
+    for s_, (a, b) in enumerate(zip(g["disps"], o["disps"])):
+        assert D.rel_err(a, b) < max(1e-5, 4 * floor[f"__disp{s_}"])
+    assert D.rel_err(g["pose"], o["pose"]) < max(1e-5, 4 * floor["__pose"])
     tier = 2e-4 if strict else 1e-2
     bad = {k: (v, floor[k]) for k, v in errs.items() if v > max(4 * floor[k], tier)}
     assert not bad, bad
 
 
-def _flat():
+def _flat(arch=18):
     import md2hip
     from md2hip.model import flux_init
-    table, total = md2hip.param_table(18, 3, (2, 3, 4, 5))
+    table, total = md2hip.param_table(arch, 3, (2, 3, 4, 5))
     return flux_init(table, total, seed=42).float().double()
 
 

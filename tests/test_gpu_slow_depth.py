@@ -1,0 +1,136 @@
+"""Config 1: ``slow_depth`` (src/simple_depth.jl:1-43) on the GPU against the CPU
+oracle's restatement (oracle/md2_oracle.py slow_depth_loss, Adam).
+
+* gradient parity of the slow_depth objective (one full-resolution scale, unweighted and
+  unnormalised smoothness, no sigmoid) at the reference's initial θ and at a textured θ, with
+  the GPU's per-pixel source choice imposed on the fp64 oracle (as in test_gpu_loss.py);
+  strict tier (affine source frames): loss rel 2e-5, gradients rel 2e-4;
+* ``md2_adam`` against the oracle's Flux ADAM rule (rel 1e-6 over three steps);
+* 8-iteration ADAM(3e-4) trajectories against the fp64 oracle loop: per-iteration loss rel
+  1e-4; from a textured start also the disparity update direction (cosine > 0.99) and the pose
+  updates (rel 2e-2).  ADAM's first steps are ~lr*sign(g), so pixels with |g| near fp32
+  rounding may legitimately step the other way; the aggregate checks are what is stable.
+"""
+import pytest
+import torch
+
+from oracle import md2_oracle as O
+from tests import _data as D
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(N, H, W, seed, strict, textured_theta):
+    import md2hip
+    x = D.triplets(N, 3, H, W, seed=seed, ramp_sources=strict)
+    K, invK = D.intrinsics(W, H)
+    sd = md2hip.SlowDepth(x.float().cuda(), K.numpy(), invK.numpy())
+    if textured_theta:
+        d = D.disparities(N, H, W, seed=seed + 4)[-1]
+        sd.disp.copy_(d.float())
+        for s, (r, t) in enumerate(D.poses(N, seed=seed + 6)):
+            sd.pose_rows[s * N:(s + 1) * N, :3] = r.float()
+            sd.pose_rows[s * N:(s + 1) * N, 3:] = t.float()
+    return sd, x, K, invK
+
+
+def _oracle_grads(sd, x, K, invK, forced_sel=None):
+    N = sd.N
+    disp = sd.disp.detach().double().cpu().clone().requires_grad_(True)
+    rows = sd.pose_rows.detach().double().cpu()
+    rv = [rows[s * N:(s + 1) * N, :3].clone().requires_grad_(True) for s in range(2)]
+    tv = [rows[s * N:(s + 1) * N, 3:].clone().requires_grad_(True) for s in range(2)]
+    per_src = []
+    loss = O.slow_depth_loss(disp, rv, tv, x, K, invK, forced_sel=forced_sel, per_source=per_src)
+    loss.backward()
+    dpose = torch.cat([torch.cat([r.grad, t.grad], 1) for r, t in zip(rv, tv)], 0)
+    return loss.detach(), disp.grad, dpose, per_src[0]
+
+
+@pytest.mark.parametrize("textured_theta", [False, True], ids=["reference-init", "textured"])
+@pytest.mark.parametrize("N,H,W", [(1, 32, 64), (1, 128, 416)])
+def test_slow_depth_gradient_parity(N, H, W, textured_theta):
+    sd, x, K, invK = _setup(N, H, W, seed=3, strict=True, textured_theta=textured_theta)
+    r = sd.evaluate(visualize=True)
+    torch.cuda.synchronize()
+    sel = r["vis_sel"][0].cpu().unsqueeze(1).long()                      # [N,1,H,W]
+    _, _, _, (l0, l1) = _oracle_grads(sd, x, K, invK)
+    tie = (l0 - l1).abs() <= 1e-4 * torch.maximum(l0, l1)
+    assert ((sel != (l1 < l0).long()) & ~tie).sum().item() == 0
+    lo, dd, dp, _ = _oracle_grads(sd, x, K, invK, forced_sel=sel)
+    assert abs(r["loss"].item() - lo.item()) <= 2e-5 * abs(lo.item())
+    if textured_theta:
+        assert D.rel_err(r["d_disp"][0].cpu(), dd) < 2e-4
+    else:
+        # reference init: constant disparity and zero translation make the warp a pure rotation,
+        # so depth cancels from the projection except through the +1e-7 of Project's divide:
+        # d loss / d disp is ~0 analytically and both sides hold rounding noise.  Bound it
+        # against the per-pixel gradient scale 1/npix instead.
+        npix = N * H * W
+        assert (r["d_disp"][0].cpu().double() - dd).abs().max().item() < 1e-4 / npix
+    assert D.rel_err(r["d_pose"].cpu(), dp) < 2e-4
+
+
+def test_adam_op_matches_flux_rule():
+    import md2hip
+    g = torch.Generator().manual_seed(9)
+    n = 10007
+    p0 = torch.randn(n, generator=g, dtype=torch.float64)
+    p = p0.float().cuda()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    ref = p0.clone()
+    opt = O.Adam(eta=3e-4)
+    for step in range(1, 4):
+        gr = torch.randn(n, generator=g, dtype=torch.float64)
+        md2hip.adam_update(p, gr.float().cuda(), m, v, step, 3e-4)
+        opt.step("p", ref, gr)
+    torch.cuda.synchronize()
+    # p ~ 1 is held in fp32 (ulp 6e-8) while three 3e-4 steps move it ~1e-3: the update itself
+    # can only be resolved to ~1e-4 relative; the parameters to 1e-7
+    assert D.rel_err(p.cpu() - p0.float(), ref - p0) < 3e-4
+    assert D.rel_err(p.cpu(), ref) < 1e-6
+
+
+def _oracle_loop(disp, rv, tv, x, K, invK, iters):
+    opt = O.Adam(eta=3e-4)
+    losses = []
+    for _ in range(iters):
+        disp.requires_grad_(True)
+        for t in rv + tv:
+            t.requires_grad_(True)
+        loss = O.slow_depth_loss(disp, rv, tv, x, K, invK)
+        loss.backward()
+        losses.append(loss.item())
+        with torch.no_grad():
+            opt.step("disp", disp, disp.grad)
+            for k, t in enumerate(rv + tv):
+                opt.step(f"p{k}", t, t.grad)
+        disp = disp.detach()
+        rv = [t.detach() for t in rv]
+        tv = [t.detach() for t in tv]
+    return disp, rv, tv, losses
+
+
+@pytest.mark.parametrize("textured_theta", [False, True], ids=["reference-init", "textured"])
+def test_slow_depth_trajectory(textured_theta):
+    """8 ADAM(3e-4) iterations vs the fp64 oracle loop.  From the reference's own init the
+    disparity gradient is rounding noise (pure rotation, see above), so ADAM's first disparity
+    steps are noise-driven there -- in the Julia reference as well -- and only the loss
+    trajectory is compared; from a textured start the disparity update direction is too."""
+    sd, x, K, invK = _setup(1, 64, 128, seed=5, strict=False, textured_theta=textured_theta)
+    disp0 = sd.disp.detach().double().cpu().clone()
+    rows = sd.pose_rows.detach().double().cpu().clone()
+    iters = 8
+    gl = [sd.step().item() for _ in range(iters)]
+    disp, rv, tv, ol = _oracle_loop(disp0.clone(), [rows[s:s + 1, :3].clone() for s in range(2)],
+                                    [rows[s:s + 1, 3:].clone() for s in range(2)], x, K, invK, iters)
+    for a, b in zip(gl, ol):
+        assert abs(a - b) <= 1e-4 * abs(b), (gl, ol)
+    if textured_theta:
+        dg = (sd.disp.detach().double().cpu() - disp0).reshape(-1)
+        do = (disp - disp0).reshape(-1)
+        cos = torch.dot(dg, do) / (dg.norm() * do.norm())
+        assert cos > 0.99, cos.item()
+        pg = sd.pose_rows.detach().double().cpu() - rows
+        po = torch.cat([torch.cat([r, t], 1) for r, t in zip(rv, tv)], 0) - rows
+        assert D.rel_err(pg, po) < 2e-2
