@@ -31,6 +31,8 @@ def is_conv3(name):
     a = targs(name)
     if a is None:
         return False
+    if "conv_px2_kernel" in name:         # <MODE, BM, BN, WM, WN, KH, KW, S, RFL>
+        return a[5] == 3 and a[8] == 0
     if "conv_px_kernel" in name:          # <MODE, TAP, BM, BN, BK, WM, WN, KH, KW, S, RFL>
         return a[7] == 3 and a[10] == 0
     if "conv_wgrad" in name:               # <BM, BN, BK, WM, WN, KH, KW, S, RFL[, CW]>
