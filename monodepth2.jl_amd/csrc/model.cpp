@@ -188,6 +188,8 @@ struct RConv {
 struct RBN {
   PBN p;
   float *mean = nullptr, *invstd = nullptr, *rmean = nullptr, *rvar = nullptr;
+  const double* part = nullptr;   // statistics partials of the current forward (bn_fwd)
+  int parts = 0;
 };
 struct EncStage {
   RConv conv;
@@ -248,6 +250,7 @@ class Model {
   float *DPRE = nullptr, *DUP = nullptr, *DO1 = nullptr;
   ConvWorkspace cws{};
   BNStatsWs bnws{};
+  long bn_slot = 0;       // doubles per partials slot (slot 1: the downsample BN of a block)
   void* tail_ws = nullptr;
   LossTailCfg tail{};
   float* loss_buf = nullptr;
@@ -463,7 +466,8 @@ class Model {
     {
       double* q;
       void* v;
-      MD2_HIP(hipMalloc(&v, std::max<long>(bnmax, 2) * sizeof(double)));
+      bn_slot = std::max<long>(bnmax, 2);
+      MD2_HIP(hipMalloc(&v, 2 * bn_slot * sizeof(double)));
       allocs.push_back(v);
       q = (double*)v;
       bnws.partials = q;
@@ -602,10 +606,26 @@ class Model {
 
   int repack(hipStream_t st) { return conv_pack_batch(pack_jobs, pack_njobs, pack_blocks, st); }
 
-  int bn_fwd(RBN& bn, const float* y, int nimg, long HW, hipStream_t st) {
+  // statistics partials only; the finalise is fused into the apply (bn_apply_fused)
+  int bn_fwd(RBN& bn, const float* y, int nimg, long HW, hipStream_t st, int slot = 0) {
     BNStatsWs w = bnws;
+    w.partials += slot * bn_slot;
     w.parts = bn_parts(bn.p.c, nimg, HW);
-    return bn_stats(y, nimg, bn.p.c, HW, 1e-5f, 0.1f, bn.mean, bn.invstd, bn.rmean, bn.rvar, w, st);
+    bn.part = w.partials;
+    bn.parts = w.parts;
+    return bn_stats_partial(y, nimg, bn.p.c, HW, w, st);
+  }
+  BNStatsIn bn_in(const RBN& bn) {
+    BNStatsIn s;
+    s.part = bn.part;
+    s.parts = bn.parts;
+    s.gamma = P(bn.p.g);
+    s.beta = P(bn.p.b);
+    s.mean = bn.mean;
+    s.invstd = bn.invstd;
+    s.run_mean = bn.rmean;
+    s.run_var = bn.rvar;
+    return s;
   }
 
   // ---- encoder forward over nimg images (input already mapped by `in`)
@@ -613,10 +633,9 @@ class Model {
     const long hw0 = (long)H0 * W0;
     MD2_TRY(conv_f(stem, nimg, in, y0, 64 * hw0, ACT_NONE, 0, st));
     MD2_TRY(bn_fwd(stem_bn, y0, nimg, hw0, st));
-    BNApply ap{};
-    ap.y = y0; ap.mean = stem_bn.mean; ap.invstd = stem_bn.invstd;
-    ap.gamma = P(stem_bn.p.g); ap.beta = P(stem_bn.p.b); ap.relu = 1;
-    MD2_TRY(bn_apply(ap, f0, nimg, 64, hw0, st));
+    BNApplyFused ap{};
+    ap.y = y0; ap.s1 = bn_in(stem_bn); ap.relu = 1;
+    MD2_TRY(bn_apply_fused(ap, f0, nimg, 64, hw0, st));
     MD2_TRY(maxpool_fwd(f0, nimg, 64, H0, W0, mp, mp_arg, Hm, Wm, st));
     for (auto& sg : stages)
       for (auto& b : sg) {
@@ -629,10 +648,9 @@ class Model {
           MD2_TRY(conv_f(e.conv, nimg, tin(x, C, HW), e.y, (long)e.conv.p.cout * ohw, ACT_NONE, 0, st));
           MD2_TRY(bn_fwd(e.bn, e.y, nimg, ohw, st));
           if (k + 1 < b.st.size()) {
-            BNApply a{};
-            a.y = e.y; a.mean = e.bn.mean; a.invstd = e.bn.invstd;
-            a.gamma = P(e.bn.p.g); a.beta = P(e.bn.p.b); a.relu = 1;
-            MD2_TRY(bn_apply(a, e.a, nimg, e.conv.p.cout, ohw, st));
+            BNApplyFused a{};
+            a.y = e.y; a.s1 = bn_in(e.bn); a.relu = 1;
+            MD2_TRY(bn_apply_fused(a, e.a, nimg, e.conv.p.cout, ohw, st));
           }
           x = e.a;
           C = e.conv.p.cout;
@@ -640,18 +658,16 @@ class Model {
         }
         EncStage& last = b.st.back();
         const long ohw = (long)b.H * b.W;
-        BNApply a{};
-        a.y = last.y; a.mean = last.bn.mean; a.invstd = last.bn.invstd;
-        a.gamma = P(last.bn.p.g); a.beta = P(last.bn.p.b); a.relu = 1;
+        BNApplyFused a{};
+        a.y = last.y; a.s1 = bn_in(last.bn); a.relu = 1;
         if (b.down) {
           MD2_TRY(conv_f(b.dconv, nimg, tin(b.in, b.Cin, (long)b.Hin * b.Win), b.yd, (long)b.C * ohw, ACT_NONE, 0, st));
-          MD2_TRY(bn_fwd(b.dbn, b.yd, nimg, ohw, st));
-          a.y2 = b.yd; a.mean2 = b.dbn.mean; a.invstd2 = b.dbn.invstd;
-          a.gamma2 = P(b.dbn.p.g); a.beta2 = P(b.dbn.p.b);
+          MD2_TRY(bn_fwd(b.dbn, b.yd, nimg, ohw, st, 1));
+          a.y2 = b.yd; a.s2 = bn_in(b.dbn);
         } else {
           a.res = b.in;
         }
-        MD2_TRY(bn_apply(a, last.a, nimg, b.C, ohw, st));
+        MD2_TRY(bn_apply_fused(a, last.a, nimg, b.C, ohw, st));
       }
     return MD2_OK;
   }
@@ -782,10 +798,9 @@ class Model {
              float* dy, float* dres, int dres_acc, hipStream_t st) {
     BNStatsWs w = bnws;
     w.parts = bn_parts(bn.p.c, nimg, HW);
-    MD2_TRY(bn_bwd_reduce(dout, mask, y, bn.mean, bn.invstd, nimg, bn.p.c, HW, Gd(bn.p.g),
-                          Gd(bn.p.b), w, st));
-    return bn_bwd_apply(dout, mask, y, bn.mean, bn.invstd, P(bn.p.g), Gd(bn.p.g), Gd(bn.p.b),
-                        nimg, bn.p.c, HW, dy, dres, dres_acc, st);
+    MD2_TRY(bn_bwd_partial(dout, mask, y, bn.mean, bn.invstd, nimg, bn.p.c, HW, w, st));
+    return bn_bwd_apply_fused(dout, mask, y, bn.mean, bn.invstd, P(bn.p.g), w, Gd(bn.p.g),
+                              Gd(bn.p.b), nimg, bn.p.c, HW, dy, dres, dres_acc, st);
   }
 
   int block_bwd(EncBlock& b, hipStream_t st) {

@@ -23,10 +23,39 @@ struct BNApply {
   int relu = 0;
 };
 int bn_apply(const BNApply& p, float* out, int N, int C, long HW, hipStream_t st);
+
+// Fused statistics finalise + apply (the model's path): bn_stats_partial writes the per-(channel,
+// image group) fp64 partials; bn_apply_fused derives mean/invstd from them inside every block
+// (same summation order as bn_stats' finalise: bit-identical), applies the affine map (+ the
+// downsample branch, residual, ReLU) and writes mean/invstd/running stats once per channel.
+struct BNStatsIn {
+  const double* part = nullptr;   // [C][parts][2] from bn_stats_partial
+  int parts = 0;
+  float eps = 1e-5f, momentum = 0.1f;
+  const float* gamma = nullptr; const float* beta = nullptr;
+  float* mean = nullptr; float* invstd = nullptr;          // [C] outputs (for the backward)
+  float* run_mean = nullptr; float* run_var = nullptr;     // running stats (nullable)
+};
+struct BNApplyFused {
+  const float* y = nullptr; BNStatsIn s1;
+  const float* y2 = nullptr; BNStatsIn s2;                 // downsample branch (nullable y2)
+  const float* res = nullptr;
+  int relu = 0;
+};
+int bn_stats_partial(const float* y, int N, int C, long HW, BNStatsWs ws, hipStream_t st);
+int bn_apply_fused(const BNApplyFused& p, float* out, int N, int C, long HW, hipStream_t st);
 // backward reduce: g = dout * (mask_out > 0 if mask_out) ; dgamma = sum g*xhat, dbeta = sum g
 int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, const float* mean,
                   const float* invstd, int N, int C, long HW, float* dgamma, float* dbeta,
                   BNStatsWs ws, hipStream_t st);
+// backward partials only (bn_bwd_reduce without its finalise); bn_bwd_apply_fused then sums the
+// partials per block (dgamma/dbeta written once per channel) and applies -- model path
+int bn_bwd_partial(const float* dout, const float* mask_out, const float* y, const float* mean,
+                   const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st);
+int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y, const float* mean,
+                       const float* invstd, const float* gamma, BNStatsWs ws, float* dgamma,
+                       float* dbeta, int N, int C, long HW, float* dy, float* dres,
+                       int dres_accumulate, hipStream_t st);
 // dy = gamma*invstd*(g - dbeta/L - xhat*dgamma/L); optional dres (=g) store/accumulate
 int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const float* mean,
                  const float* invstd, const float* gamma, const float* dgamma,

@@ -81,6 +81,21 @@ __global__ void bn_stats_final_kernel(const double* __restrict__ part, int C, in
   }
 }
 
+int bn_stats_partial(const float* y, int N, int C, long HW, BNStatsWs ws, hipStream_t st) {
+  MD2_TRY(check_u31((long)N * C * HW));
+  MD2_CHECK_ARG(ws.parts >= 1 && ws.parts <= N, "bn_stats: parts must split the images");
+  const int vec = HW % 4 == 0;
+  const FastDiv fdu = fd(vec ? HW / 4 : HW);
+  if (vec)
+    hipLaunchKernelGGL(bn_stats_partial_kernel<true>, dim3(C, ws.parts), dim3(256), 0, st, y, C,
+                       (int)HW, N, ws.parts, fdu, ws.partials);
+  else
+    hipLaunchKernelGGL(bn_stats_partial_kernel<false>, dim3(C, ws.parts), dim3(256), 0, st, y, C,
+                       (int)HW, N, ws.parts, fdu, ws.partials);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 int bn_stats(const float* y, int N, int C, long HW, float eps, float momentum, float* mean,
              float* invstd, float* run_mean, float* run_var, BNStatsWs ws, hipStream_t st) {
   MD2_TRY(check_u31((long)N * C * HW));
@@ -159,6 +174,106 @@ int bn_apply(const BNApply& p, float* out, int N, int C, long HW, hipStream_t st
   return MD2_OK;
 }
 
+
+// ---- fused finalise + apply.  A block covers 256 consecutive units (float4 or scalar), i.e. the
+// planes pl0..pl1 (plane = image*C + channel, <= 256 of them); thread t < #planes finalises the
+// channel of plane pl0+t from the partials in exactly bn_stats_final_kernel's order and
+// arithmetic (so mean/invstd are bit-identical to the two-kernel path), the scale/shift go
+// through LDS.  The block holding the first unit of image 0's plane of channel c writes mean[c],
+// invstd[c] and the running statistics.
+__device__ __forceinline__ void bn_finalise_plane(const BNStatsIn& s, int c, double total,
+                                                  bool owner, float& sc, float& sh) {
+  double a = 0.0, aa = 0.0;
+  const double* q = s.part + (long)c * s.parts * 2;
+  for (int p = 0; p < s.parts; ++p) {
+    a += q[2 * p];
+    aa += q[2 * p + 1];
+  }
+  const double mu = a / total;
+  const double var = fmax(aa / total - mu * mu, 0.0);
+  const float meanf = (float)mu;
+  const float isf = (float)(1.0 / sqrt(var + (double)s.eps));
+  sc = s.gamma[c] * isf;
+  sh = s.beta[c] - meanf * sc;
+  if (owner) {
+    s.mean[c] = meanf;
+    s.invstd[c] = isf;
+    if (s.run_mean) {
+      const float m = s.momentum;
+      s.run_mean[c] = (1.f - m) * s.run_mean[c] + m * meanf;
+      s.run_var[c] = (1.f - m) * s.run_var[c] + m * (float)(var * total / fmax(total - 1.0, 1.0));
+    }
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNApplyFused p, float* __restrict__ out,
+                                                             uint32_t nu, FastDiv fdU, FastDiv fdC,
+                                                             double total) {
+  __shared__ float s_sc[256], s_sh[256], s_sc2[256], s_sh2[256];
+  const uint32_t u0 = blockIdx.x * 256u;
+  const uint32_t pl0 = fdiv(u0, fdU);
+  const uint32_t npl = fdiv(min(u0 + 255u, nu - 1u), fdU) - pl0 + 1u;
+  if (threadIdx.x < npl) {
+    const uint32_t pl = pl0 + threadIdx.x;
+    const int c = (int)(pl - fdiv(pl, fdC) * fdC.d);
+    const bool owner = pl < fdC.d && pl * fdU.d >= u0;
+    bn_finalise_plane(p.s1, c, total, owner, s_sc[threadIdx.x], s_sh[threadIdx.x]);
+    if (p.y2) bn_finalise_plane(p.s2, c, total, owner, s_sc2[threadIdx.x], s_sh2[threadIdx.x]);
+  }
+  __syncthreads();
+  const uint32_t u = u0 + threadIdx.x;
+  if (u >= nu) return;
+  const uint32_t li = fdiv(u, fdU) - pl0;
+  const float sc = s_sc[li], sh = s_sh[li];
+  float sc2 = 0.f, sh2 = 0.f;
+  if (p.y2) {
+    sc2 = s_sc2[li];
+    sh2 = s_sh2[li];
+  }
+  if (VEC) {
+    const long i = 4L * u;
+    float4 v = *reinterpret_cast<const float4*>(p.y + i);
+    float r[4] = {v.x * sc + sh, v.y * sc + sh, v.z * sc + sh, v.w * sc + sh};
+    if (p.y2) {
+      const float4 q = *reinterpret_cast<const float4*>(p.y2 + i);
+      r[0] += q.x * sc2 + sh2; r[1] += q.y * sc2 + sh2; r[2] += q.z * sc2 + sh2; r[3] += q.w * sc2 + sh2;
+    }
+    if (p.res) {
+      const float4 q = *reinterpret_cast<const float4*>(p.res + i);
+      r[0] += q.x; r[1] += q.y; r[2] += q.z; r[3] += q.w;
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = fmaxf(r[k], 0.f);
+    }
+    *reinterpret_cast<float4*>(out + i) = make_float4(r[0], r[1], r[2], r[3]);
+  } else {
+    float r = p.y[u] * sc + sh;
+    if (p.y2) r += p.y2[u] * sc2 + sh2;
+    if (p.res) r += p.res[u];
+    if (p.relu) r = fmaxf(r, 0.f);
+    out[u] = r;
+  }
+}
+
+int bn_apply_fused(const BNApplyFused& p, float* out, int N, int C, long HW, hipStream_t st) {
+  const long n = (long)N * C * HW;
+  MD2_TRY(check_u31(n));
+  MD2_CHECK_ARG(p.s1.part && p.s1.parts >= 1 && (!p.y2 || (p.s2.part && p.s2.parts >= 1)),
+                "bn_apply_fused: missing statistics partials");
+  const double total = (double)((long)N * HW);
+  if (HW % 4 == 0) {
+    hipLaunchKernelGGL(bn_apply_fused_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st, p,
+                       out, (uint32_t)(n / 4), fd(HW / 4), fd(C), total);
+  } else {
+    hipLaunchKernelGGL(bn_apply_fused_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st, p, out,
+                       (uint32_t)n, fd(HW), fd(C), total);
+  }
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
@@ -221,6 +336,22 @@ __global__ void bn_bwd_final_kernel(const double* __restrict__ part, int C, int 
   }
   dbeta[c] = (float)sg;
   dgamma[c] = (float)sgx;
+}
+
+int bn_bwd_partial(const float* dout, const float* mask_out, const float* y, const float* mean,
+                   const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st) {
+  MD2_TRY(check_u31((long)N * C * HW));
+  MD2_CHECK_ARG(ws.parts >= 1 && ws.parts <= N, "bn_bwd: parts must split the images");
+  const int vec = HW % 4 == 0;
+  const FastDiv fdu = fd(vec ? HW / 4 : HW);
+  if (vec)
+    hipLaunchKernelGGL(bn_bwd_partial_kernel<true>, dim3(C, ws.parts), dim3(256), 0, st, dout,
+                       mask_out, y, mean, invstd, C, (int)HW, N, ws.parts, fdu, ws.partials);
+  else
+    hipLaunchKernelGGL(bn_bwd_partial_kernel<false>, dim3(C, ws.parts), dim3(256), 0, st, dout,
+                       mask_out, y, mean, invstd, C, (int)HW, N, ws.parts, fdu, ws.partials);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
 }
 
 int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, const float* mean,
@@ -312,6 +443,109 @@ int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const
     hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st, dout,
                        mask_out, y, mean, invstd, gamma, dgamma, dbeta, (uint32_t)n, fd(HW), fd(C),
                        invL, dy, dres, dres_accumulate);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+
+// ---- fused finalise + backward apply: per block the channels of its planes sum the backward
+// partials in bn_bwd_final_kernel's order (bit-identical dgamma/dbeta), the owner block of each
+// channel (first unit of image 0's plane) stores dgamma[c]/dbeta[c].
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
+    const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, const double* __restrict__ part, int parts,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, uint32_t nu, FastDiv fdU, FastDiv fdC,
+    float invL, float* __restrict__ dy, float* __restrict__ dres, int dres_acc) {
+  __shared__ float s_k0[256], s_db[256], s_dg[256], s_mu[256], s_is[256];
+  const uint32_t u0 = blockIdx.x * 256u;
+  const uint32_t pl0 = fdiv(u0, fdU);
+  const uint32_t npl = fdiv(min(u0 + 255u, nu - 1u), fdU) - pl0 + 1u;
+  if (threadIdx.x < npl) {
+    const uint32_t pl = pl0 + threadIdx.x;
+    const int c = (int)(pl - fdiv(pl, fdC) * fdC.d);
+    double sg = 0.0, sgx = 0.0;
+    const double* q = part + (long)c * parts * 2;
+    for (int p = 0; p < parts; ++p) {
+      sg += q[2 * p];
+      sgx += q[2 * p + 1];
+    }
+    const float dbf = (float)sg, dgf = (float)sgx;
+    if (pl < fdC.d && pl * fdU.d >= u0) {
+      dbeta[c] = dbf;
+      dgamma[c] = dgf;
+    }
+    const float is = invstd[c];
+    s_k0[threadIdx.x] = gamma[c] * is;
+    s_db[threadIdx.x] = dbf * invL;
+    s_dg[threadIdx.x] = dgf * invL;
+    s_mu[threadIdx.x] = mean[c];
+    s_is[threadIdx.x] = is;
+  }
+  __syncthreads();
+  const uint32_t u = u0 + threadIdx.x;
+  if (u >= nu) return;
+  const uint32_t li = fdiv(u, fdU) - pl0;
+  const float k0 = s_k0[li], db = s_db[li], dg = s_dg[li], mu = s_mu[li], is = s_is[li];
+  if (VEC) {
+    const long i = 4L * u;
+    float g[4];
+    {
+      const float4 t = *reinterpret_cast<const float4*>(dout + i);
+      g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
+    }
+    if (mask) {
+      const float4 m = *reinterpret_cast<const float4*>(mask + i);
+      if (!(m.x > 0.f)) g[0] = 0.f;
+      if (!(m.y > 0.f)) g[1] = 0.f;
+      if (!(m.z > 0.f)) g[2] = 0.f;
+      if (!(m.w > 0.f)) g[3] = 0.f;
+    }
+    const float4 v = *reinterpret_cast<const float4*>(y + i);
+    const float yv[4] = {v.x, v.y, v.z, v.w};
+    float r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = k0 * (g[k] - db - (yv[k] - mu) * is * dg);
+    *reinterpret_cast<float4*>(dy + i) = make_float4(r[0], r[1], r[2], r[3]);
+    if (dres) {
+      float4 o = make_float4(g[0], g[1], g[2], g[3]);
+      if (dres_acc) {
+        const float4 q = *reinterpret_cast<const float4*>(dres + i);
+        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+      }
+      *reinterpret_cast<float4*>(dres + i) = o;
+    }
+  } else {
+    float g = dout[u];
+    if (mask && !(mask[u] > 0.f)) g = 0.f;
+    const float xh = (y[u] - mu) * is;
+    dy[u] = k0 * (g - db - xh * dg);
+    if (dres) {
+      if (dres_acc)
+        dres[u] += g;
+      else
+        dres[u] = g;
+    }
+  }
+}
+
+int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y, const float* mean,
+                       const float* invstd, const float* gamma, BNStatsWs ws, float* dgamma,
+                       float* dbeta, int N, int C, long HW, float* dy, float* dres,
+                       int dres_accumulate, hipStream_t st) {
+  const long n = (long)N * C * HW;
+  MD2_TRY(check_u31(n));
+  MD2_CHECK_ARG(ws.partials && ws.parts >= 1, "bn_bwd_apply_fused: missing partials");
+  const float invL = 1.f / (float)((long)N * HW);
+  if (HW % 4 == 0)
+    hipLaunchKernelGGL(bn_bwd_apply_fused_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st,
+                       dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
+                       (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy, dres, dres_accumulate);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_fused_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st,
+                       dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
+                       (uint32_t)n, fd(HW), fd(C), invL, dy, dres, dres_accumulate);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
