@@ -240,8 +240,14 @@ __global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __r
   *d = accumulate ? *d + v : v;
 }
 
-// pixels per partial block: ~2 per lane, at most 2048 partials
-int head_parts(long npix) { return (int)std::min<long>(std::max<long>(cdiv(npix, 256 * 2), 1), 2048); }
+// pixels per partial block: ~8 per lane (the 73-accumulator block reduction is amortised over
+// them), raised toward >= 512 blocks (parts x channel groups) while every lane keeps a pixel
+int head_parts(long npix, int Cin) {
+  const long groups = cdiv(Cin, HEAD_CG);
+  long parts = std::max<long>(cdiv(npix, 256 * 8), 1);
+  parts = std::max(parts, std::min<long>(cdiv(512, groups), cdiv(npix, 256)));
+  return (int)std::min<long>(parts, 2048);
+}
 
 // channel groups (log2) so a launch has >= ~128k lanes, each group keeping >= 4 channels
 int head_cg_shift(long npix, int Cin) {
@@ -258,7 +264,7 @@ bool head_conv_ok(const ConvShape& s) {
 }
 
 size_t head_wgrad_workspace(const ConvShape& s) {
-  return (size_t)head_parts((long)s.N * s.H * s.W) * (s.Cin * 9 + 1) * sizeof(float);
+  return (size_t)head_parts((long)s.N * s.H * s.W, s.Cin) * (s.Cin * 9 + 1) * sizeof(float);
 }
 
 int head_fwd(const ConvShape& s, const HeadIn& x, HeadW w, const float* bias, int act, float* y,
@@ -296,7 +302,7 @@ int head_dgrad(const ConvShape& s, const float* dy, HeadW w, float* dx, long dxb
 int head_wgrad(const ConvShape& s, const HeadIn& x, const float* dy, float* dw, float* db,
                int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
   const long np = (long)s.N * s.H * s.W;
-  const int parts = head_parts(np);
+  const int parts = head_parts(np, s.Cin);
   MD2_CHECK_ARG(ws && ws_bytes >= head_wgrad_workspace(s), "head_wgrad workspace");
   float* part = (float*)ws;
   const uint32_t npix = (uint32_t)np;

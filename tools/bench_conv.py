@@ -17,7 +17,16 @@ SH = [  # name, x_shape, cout, k, s, p, reflect
     ("d5c2", (12, 16, 128, 416), 16, 3, 1, 1, 1),
     ("d4c2", (12, 96, 64, 208), 32, 3, 1, 1, 1),
     ("d3c2", (12, 128, 32, 104), 64, 3, 1, 1, 1),
+    ("d5c1", (12, 32, 64, 208), 16, 3, 1, 1, 1),
+    ("d4c1", (12, 64, 32, 104), 32, 3, 1, 1, 1),
+    ("h5", (12, 16, 128, 416), 1, 3, 1, 1, 1),
+    ("h4", (12, 32, 64, 208), 1, 3, 1, 1, 1),
+    ("h3", (12, 64, 32, 104), 1, 3, 1, 1, 1),
+    ("h2", (12, 128, 16, 52), 1, 3, 1, 1, 1),
 ]
+_only = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--only=")]
+if _only:
+    SH = [t for t in SH if t[0] in _only[0]]
 def timeit(fn, it=20):
     for _ in range(3): fn()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -42,4 +51,10 @@ for name, xs, cout, k, st, pd, rf in SH:
     tf, tg, th = timeit(f), timeit(g), timeit(h)
     tot["fwd"] += tf; tot["dgrad"] += tg; tot["wgrad"] += th
     print(f"{name:6s} GF {flops/1e9:7.2f}  fwd {tf*1e3:8.1f}us {flops/tf/1e9:6.1f}TF  dgrad {tg*1e3:8.1f}us {flops/tg/1e9:6.1f}TF  wgrad {th*1e3:8.1f}us {flops/th/1e9:6.1f}TF", flush=True)
+    if "--miopen" in sys.argv and not rf:   # MIOpen (torch conv, exact fp32) at the same shape
+        wt = w.clone()
+        tf2 = timeit(lambda: torch.nn.functional.conv2d(x, wt, None, st, pd))
+        cb = lambda m: torch.ops.aten.convolution_backward(dy, x, wt, None, [st, st], [pd, pd], [1, 1], False, [0, 0], 1, m)
+        tg2, th2 = timeit(lambda: cb([True, False, False])), timeit(lambda: cb([False, True, False]))
+        print(f"{'miopen':6s} {'':10s}  fwd {tf2*1e3:8.1f}us {flops/tf2/1e9:6.1f}TF  dgrad {tg2*1e3:8.1f}us {flops/tg2/1e9:6.1f}TF  wgrad {th2*1e3:8.1f}us {flops/th2/1e9:6.1f}TF", flush=True)
 print(tot)
