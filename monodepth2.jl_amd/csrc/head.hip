@@ -167,18 +167,20 @@ __global__ __launch_bounds__(256) void head_wgrad_partial_kernel(HeadIn x, const
                                                                  FastDiv fdH, uint32_t npix,
                                                                  float* __restrict__ part) {
   __shared__ float s_red[4][HEAD_CG * 9 + 1];
+  __shared__ double s_dred[4];
   const int c0 = blockIdx.y * HEAD_CG;
   const int ncg = min(HEAD_CG, Cin - c0);
   float acc[HEAD_CG * 9 + 1];
 #pragma unroll
   for (int t = 0; t < HEAD_CG * 9 + 1; ++t) acc[t] = 0.f;
+  double gsum = 0.0;   // bias gradient in fp64 (a long cancelling sum)
   const long HW = (long)H * W;
   const uint32_t stride = gridDim.x * 256;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < npix; i += stride) {
     const uint32_t r = fdiv(i, fdW), b = fdiv(r, fdH);
     const int px = (int)(i - r * fdW.d), py = (int)(r - b * fdH.d);
     const float g = dy[i];
-    acc[HEAD_CG * 9] += g;
+    gsum += (double)g;
     int ro[3], co[3];
     bool rv[3], cv[3];
 #pragma unroll
@@ -206,18 +208,20 @@ __global__ __launch_bounds__(256) void head_wgrad_partial_kernel(HeadIn x, const
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-  for (int t = 0; t < HEAD_CG * 9 + 1; ++t) {
+  for (int t = 0; t < HEAD_CG * 9; ++t) {
     const float v = wave_sum(acc[t]);
     if (lane == 0) s_red[wv][t] = v;
+  }
+  {
+    const double v = wave_sum_d(gsum);
+    if (lane == 0) s_dred[wv] = v;
   }
   __syncthreads();
   float* dst = part + (long)blockIdx.x * (Cin * 9 + 1);
   for (int t = threadIdx.x; t < ncg * 9; t += 256)
     dst[c0 * 9 + t] = (s_red[0][t] + s_red[1][t]) + (s_red[2][t] + s_red[3][t]);
-  if (blockIdx.y == 0 && threadIdx.x == 0) {
-    const int t = HEAD_CG * 9;
-    dst[Cin * 9] = (s_red[0][t] + s_red[1][t]) + (s_red[2][t] + s_red[3][t]);
-  }
+  if (blockIdx.y == 0 && threadIdx.x == 0)
+    dst[Cin * 9] = (float)((s_dred[0] + s_dred[1]) + (s_dred[2] + s_dred[3]));
 }
 
 // pass 2: one block per column (Cin*9 weights + the bias), fixed-order tree over the partials
@@ -256,6 +260,281 @@ int head_cg_shift(long npix, int Cin) {
   return sh;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Column-strip kernels for the wide heads (W >= 64): lane = one image column of a 64-column
+// segment, walking R consecutive rows with the three input rows of the 3x3 window held in
+// registers, so each input value is loaded once per column offset (3 loads per pixel and channel
+// instead of 9).  A unit = (image, row band, column segment).
+// ---------------------------------------------------------------------------------------------
+struct StripGeo {
+  int H, W, nseg, nband;
+};
+
+__device__ __forceinline__ void strip_unit(const StripGeo& g, int u, int R, int& b, int& y0, int& xx) {
+  const int seg = u % g.nseg;
+  u /= g.nseg;
+  const int band = u % g.nband;
+  b = u / g.nband;
+  y0 = band * R;
+  xx = seg * 64 + (threadIdx.x & 63);
+}
+
+// one input row (reflect / zero padded) at the three column offsets of this lane
+template <bool RFL>
+__device__ __forceinline__ void strip_row(const float* __restrict__ xc, int yy, int H, int W,
+                                          const int (&co)[3], const bool (&cv)[3], float (&v)[3]) {
+  int sy = src_of<RFL>(yy, 1, H);
+  const bool rv = sy >= 0;
+  sy = min(max(sy, 0), H - 1);   // rows past the band end (never stored) stay in bounds
+#pragma unroll
+  for (int k = 0; k < 3; ++k) v[k] = (RFL || (rv && cv[k])) ? xc[sy * W + co[k]] : 0.f;
+}
+
+template <bool RFL>
+__device__ __forceinline__ void strip_cols(int xx, int W, int (&co)[3], bool (&cv)[3]) {
+  const int xc = min(xx, W - 1);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int sx = src_of<RFL>(xc, k, W);
+    cv[k] = sx >= 0;
+    co[k] = min(max(sx, 0), W - 1);
+  }
+}
+
+// forward: the block's 4 waves split the channels; partial columns summed in wave order (LDS)
+template <bool RFL, int R>
+__global__ __launch_bounds__(256) void head_fwd_strip_kernel(HeadIn x, HeadW w, int Cin, StripGeo g,
+                                                             const float* __restrict__ bias, int act,
+                                                             float* __restrict__ y, long ybs,
+                                                             int accumulate) {
+  __shared__ float s_part[3][R][64];
+  const int lane = threadIdx.x & 63, wq = threadIdx.x >> 6;
+  int b, y0, xx;
+  strip_unit(g, blockIdx.x, R, b, y0, xx);
+  int co[3];
+  bool cv[3];
+  strip_cols<RFL>(xx, g.W, co, cv);
+  const long HW = (long)g.H * g.W;
+  const float* xb = x.p + img_off(x, b);
+  const int cpw = (Cin + 3) >> 2;
+  const int cb = wq * cpw, ce = min(Cin, cb + cpw);
+  float out[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) out[r] = 0.f;
+  for (int c = cb; c < ce; ++c) {
+    const float* xc = xb + c * HW;
+    float wt[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[t] = w.p[(long)c * w.sc + (long)t * w.st];
+    float a0[3], a1[3], a2[3];
+    strip_row<RFL>(xc, y0 - 1, g.H, g.W, co, cv, a0);
+    strip_row<RFL>(xc, y0, g.H, g.W, co, cv, a1);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      strip_row<RFL>(xc, y0 + r + 1, g.H, g.W, co, cv, a2);
+      float v = out[r];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        v = fmaf(wt[k], a0[k], v);
+        v = fmaf(wt[3 + k], a1[k], v);
+        v = fmaf(wt[6 + k], a2[k], v);
+      }
+      out[r] = v;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        a0[k] = a1[k];
+        a1[k] = a2[k];
+      }
+    }
+  }
+  if (wq > 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) s_part[wq - 1][r][lane] = out[r];
+  }
+  __syncthreads();
+  if (wq > 0 || xx >= g.W) return;
+  const float bb = bias ? bias[0] : 0.f;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (y0 + r >= g.H) break;
+    float v = ((out[r] + s_part[0][r][lane]) + s_part[1][r][lane]) + s_part[2][r][lane];
+    v = act_f(v + bb, act);
+    float* dst = y + (long)b * ybs + (long)(y0 + r) * g.W + xx;
+    *dst = accumulate ? *dst + v : v;
+  }
+}
+
+// filter gradient partials: wave wq of channel block blockIdx.y owns CPW channels; per unit a row
+// [Cin*9 + 1] of partials (the last column = sum of dy, the bias gradient)
+template <bool RFL, int R, int CPW>
+__global__ __launch_bounds__(256) void head_wgrad_strip_kernel(HeadIn x, const float* __restrict__ dy,
+                                                               int Cin, StripGeo g,
+                                                               float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wq = threadIdx.x >> 6;
+  int b, y0, xx;
+  strip_unit(g, blockIdx.x, R, b, y0, xx);
+  int co[3];
+  bool cv[3];
+  strip_cols<RFL>(xx, g.W, co, cv);
+  const bool live = xx < g.W;
+  const long HW = (long)g.H * g.W;
+  float gr[R];
+  double gs = 0.0;   // bias gradient in fp64: a long cancelling sum
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    gr[r] = (live && y0 + r < g.H) ? dy[(long)b * HW + (long)(y0 + r) * g.W + xx] : 0.f;
+    gs += (double)gr[r];
+  }
+  const int c0 = (blockIdx.y * 4 + wq) * CPW;
+  const float* xb = x.p + img_off(x, b);
+  float acc[CPW][9];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) {
+    if (c0 + i < Cin) {
+      const float* xc = xb + (c0 + i) * HW;
+      float a0[3], a1[3], a2[3];
+      strip_row<RFL>(xc, y0 - 1, g.H, g.W, co, cv, a0);
+      strip_row<RFL>(xc, y0, g.H, g.W, co, cv, a1);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        strip_row<RFL>(xc, y0 + r + 1, g.H, g.W, co, cv, a2);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          acc[i][k] = fmaf(gr[r], a0[k], acc[i][k]);
+          acc[i][3 + k] = fmaf(gr[r], a1[k], acc[i][3 + k]);
+          acc[i][6 + k] = fmaf(gr[r], a2[k], acc[i][6 + k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          a0[k] = a1[k];
+          a1[k] = a2[k];
+        }
+      }
+    }
+  }
+  float* dst = part + (long)blockIdx.x * (Cin * 9 + 1);
+#pragma unroll
+  for (int i = 0; i < CPW; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float v = wave_sum(acc[i][t]);
+      if (lane == 0 && c0 + i < Cin) dst[(c0 + i) * 9 + t] = v;
+    }
+  if (blockIdx.y == 0 && wq == 0) {
+    const double v = wave_sum_d(gs);
+    if (lane == 0) dst[Cin * 9] = (float)v;
+  }
+}
+
+// data gradient: one unit per WAVE, all channels per lane.  E(yy) = the dy row yy at the three
+// column taps with the reflect folds (q = 1 also takes p = 0 through tap 0, q = W-2 takes p = W-1
+// through tap 2); D = rows E(qy+1), E(qy), E(qy-1) with the same folds in y; dx[c] = w[c] . D.
+template <bool RFL>
+__device__ __forceinline__ void strip_erow(const float* __restrict__ g, int yy, int H, int W, int qx,
+                                           float (&e)[3]) {
+  const bool rv = yy >= 0 && yy < H;
+  const int sy = min(max(yy, 0), H - 1);
+  const float* row = g + (long)sy * W;
+  const int xq = min(qx, W - 1);
+  e[0] = (rv && xq + 1 < W) ? row[xq + 1] : 0.f;
+  e[1] = rv ? row[xq] : 0.f;
+  e[2] = (rv && xq >= 1) ? row[xq - 1] : 0.f;
+  if (RFL) {
+    if (xq == 1 && rv) e[0] += row[0];
+    if (xq == W - 2 && rv) e[2] += row[W - 1];
+  }
+}
+
+template <bool RFL, int R>
+__global__ __launch_bounds__(256) void head_dgrad_strip_kernel(const float* __restrict__ dy, HeadW w,
+                                                               int Cin, StripGeo g, int nunits,
+                                                               float* __restrict__ dx, long dxbs,
+                                                               int accumulate) {
+  const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= nunits) return;
+  int b, y0, qx;
+  strip_unit(g, u, R, b, y0, qx);
+  const long HW = (long)g.H * g.W;
+  const float* gb = dy + (long)b * HW;
+  float D[R][9];
+  float e0[3], e1[3], e2[3];   // E(y+1), E(y), E(y-1) of the current row y
+  strip_erow<RFL>(gb, y0 + 1, g.H, g.W, qx, e0);
+  strip_erow<RFL>(gb, y0, g.H, g.W, qx, e1);
+  strip_erow<RFL>(gb, y0 - 1, g.H, g.W, qx, e2);
+  float ef0[3] = {0.f, 0.f, 0.f}, efH[3] = {0.f, 0.f, 0.f};
+  if (RFL) {
+    if (y0 <= 1 && 1 < y0 + R) strip_erow<RFL>(gb, 0, g.H, g.W, qx, ef0);
+    if (y0 <= g.H - 2 && g.H - 2 < y0 + R) strip_erow<RFL>(gb, g.H - 1, g.H, g.W, qx, efH);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int qy = y0 + r;
+    const bool f0 = RFL && qy == 1, fH = RFL && qy == g.H - 2;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      D[r][k] = e0[k] + (f0 ? ef0[k] : 0.f);
+      D[r][3 + k] = e1[k];
+      D[r][6 + k] = e2[k] + (fH ? efH[k] : 0.f);
+    }
+    if (r + 1 < R) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        e2[k] = e1[k];
+        e1[k] = e0[k];
+      }
+      strip_erow<RFL>(gb, qy + 2, g.H, g.W, qx, e0);
+    }
+  }
+  if (qx >= g.W) return;
+  float* out = dx + (long)b * dxbs + (long)y0 * g.W + qx;
+  const int cpg = (Cin + gridDim.y - 1) / gridDim.y;
+  const int cb = blockIdx.y * cpg, ce = min(Cin, cb + cpg);
+  for (int c = cb; c < ce; ++c) {
+    float wt[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[t] = w.p[(long)c * w.sc + (long)t * w.st];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (y0 + r >= g.H) break;
+      float v = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) v = fmaf(wt[t], D[r][t], v);
+      float* d = out + c * HW + (long)r * g.W;
+      *d = accumulate ? *d + v : v;
+    }
+  }
+}
+
+StripGeo strip_geo(const ConvShape& s, int R) {
+  StripGeo g;
+  g.H = s.H;
+  g.W = s.W;
+  g.nseg = cdiv(s.W, 64);
+  g.nband = cdiv(s.H, R);
+  return g;
+}
+long strip_units(const ConvShape& s, int R) { return (long)s.N * cdiv(s.H, R) * cdiv(s.W, 64); }
+
+// strip path for the wide heads; MD2_HEAD_STRIP=0 keeps the pixel-per-lane kernels
+bool strip_ok(const ConvShape& s) {
+  static const int on = [] {
+    const char* e = getenv("MD2_HEAD_STRIP");
+    return e ? atoi(e) : 1;
+  }();
+  return on && s.W >= 64 && s.H >= 4;
+}
+// forward / filter gradient strips only where they give enough blocks (measured: head5, head4;
+// the head3 grid of 96-192 blocks ran slower than the pixel-per-lane kernels)
+bool strip_fw_ok(const ConvShape& s) { return strip_ok(s) && (long)s.N * s.H * s.W >= 131072; }
+// rows per lane: 16 when that still gives >= 512 units, else 8
+int strip_rows(const ConvShape& s) { return strip_units(s, 16) >= 512 ? 16 : 8; }
+// wgrad channels per wave (8 for Cin >= 32) and channel blocks
+int strip_cpw(int Cin) { return Cin >= 32 ? 8 : 4; }
 }  // namespace
 
 bool head_conv_ok(const ConvShape& s) {
@@ -264,11 +543,29 @@ bool head_conv_ok(const ConvShape& s) {
 }
 
 size_t head_wgrad_workspace(const ConvShape& s) {
-  return (size_t)head_parts((long)s.N * s.H * s.W, s.Cin) * (s.Cin * 9 + 1) * sizeof(float);
+  long parts = head_parts((long)s.N * s.H * s.W, s.Cin);
+  if (strip_fw_ok(s)) parts = std::max(parts, strip_units(s, strip_rows(s)));
+  return (size_t)parts * (s.Cin * 9 + 1) * sizeof(float);
 }
 
 int head_fwd(const ConvShape& s, const HeadIn& x, HeadW w, const float* bias, int act, float* y,
              long ybs, int accumulate, hipStream_t st) {
+  if (strip_fw_ok(s)) {
+    const int R = strip_rows(s);
+    const StripGeo g = strip_geo(s, R);
+    const dim3 grid((unsigned)strip_units(s, R));
+#define MD2_HF(RF, RR)                                                                             \
+  hipLaunchKernelGGL((head_fwd_strip_kernel<RF, RR>), grid, dim3(256), 0, st, x, w, s.Cin, g, bias, \
+                     act, y, ybs, accumulate)
+    if (s.reflect) {
+      if (R == 16) MD2_HF(true, 16); else MD2_HF(true, 8);
+    } else {
+      if (R == 16) MD2_HF(false, 16); else MD2_HF(false, 8);
+    }
+#undef MD2_HF
+    MD2_LAUNCH_CHECK();
+    return MD2_OK;
+  }
   const uint32_t npix = (uint32_t)((long)s.N * s.H * s.W);
   const FastDiv fdW = make_fastdiv(s.W), fdH = make_fastdiv(s.H);
   const int sh = head_cg_shift(npix, s.Cin);
@@ -285,6 +582,22 @@ int head_fwd(const ConvShape& s, const HeadIn& x, HeadW w, const float* bias, in
 
 int head_dgrad(const ConvShape& s, const float* dy, HeadW w, float* dx, long dxbs, int accumulate,
                hipStream_t st) {
+  if (strip_ok(s)) {
+    constexpr int R = 4;
+    const StripGeo g = strip_geo(s, R);
+    const long nu = strip_units(s, R);
+    // channel groups (each re-forms D) until ~4096 waves, >= 4 channels per group
+    const int G = (int)std::max<long>(1, std::min<long>(cdiv(4096, nu), s.Cin / 4));
+    const dim3 grid((unsigned)cdiv(nu, 4), G);
+    if (s.reflect)
+      hipLaunchKernelGGL((head_dgrad_strip_kernel<true, R>), grid, dim3(256), 0, st, dy, w, s.Cin, g,
+                         (int)nu, dx, dxbs, accumulate);
+    else
+      hipLaunchKernelGGL((head_dgrad_strip_kernel<false, R>), grid, dim3(256), 0, st, dy, w, s.Cin, g,
+                         (int)nu, dx, dxbs, accumulate);
+    MD2_LAUNCH_CHECK();
+    return MD2_OK;
+  }
   const uint32_t npix = (uint32_t)((long)s.N * s.H * s.W);
   const FastDiv fdW = make_fastdiv(s.W), fdH = make_fastdiv(s.H);
   const int sh = head_cg_shift(npix, s.Cin);
@@ -301,10 +614,32 @@ int head_dgrad(const ConvShape& s, const float* dy, HeadW w, float* dx, long dxb
 
 int head_wgrad(const ConvShape& s, const HeadIn& x, const float* dy, float* dw, float* db,
                int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
-  const long np = (long)s.N * s.H * s.W;
-  const int parts = head_parts(np, s.Cin);
   MD2_CHECK_ARG(ws && ws_bytes >= head_wgrad_workspace(s), "head_wgrad workspace");
   float* part = (float*)ws;
+  const int ncols = s.Cin * 9;
+  if (strip_fw_ok(s)) {
+    const int R = strip_rows(s), cpw = strip_cpw(s.Cin);
+    const StripGeo g = strip_geo(s, R);
+    const long nu = strip_units(s, R);
+    const dim3 grid((unsigned)nu, cdiv(s.Cin, 4 * cpw));
+#define MD2_HW(RF, RR, CP)                                                                         \
+  hipLaunchKernelGGL((head_wgrad_strip_kernel<RF, RR, CP>), grid, dim3(256), 0, st, x, dy, s.Cin, g, part)
+    if (s.reflect) {
+      if (R == 16) { if (cpw == 8) MD2_HW(true, 16, 8); else MD2_HW(true, 16, 4); }
+      else { if (cpw == 8) MD2_HW(true, 8, 8); else MD2_HW(true, 8, 4); }
+    } else {
+      if (R == 16) { if (cpw == 8) MD2_HW(false, 16, 8); else MD2_HW(false, 16, 4); }
+      else { if (cpw == 8) MD2_HW(false, 8, 8); else MD2_HW(false, 8, 4); }
+    }
+#undef MD2_HW
+    MD2_LAUNCH_CHECK();
+    hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3(ncols + 1), dim3(256), 0, st, part, (int)nu,
+                       ncols, dw, db, accumulate);
+    MD2_LAUNCH_CHECK();
+    return MD2_OK;
+  }
+  const long np = (long)s.N * s.H * s.W;
+  const int parts = head_parts(np, s.Cin);
   const uint32_t npix = (uint32_t)np;
   const FastDiv fdW = make_fastdiv(s.W), fdH = make_fastdiv(s.H);
   const dim3 grid(parts, cdiv(s.Cin, HEAD_CG));
@@ -315,7 +650,6 @@ int head_wgrad(const ConvShape& s, const HeadIn& x, const float* dy, float* dw, 
     hipLaunchKernelGGL(head_wgrad_partial_kernel<false>, grid, dim3(256), 0, st, x, dy, s.Cin, s.H,
                        s.W, fdW, fdH, npix, part);
   MD2_LAUNCH_CHECK();
-  const int ncols = s.Cin * 9;
   hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3(ncols + 1), dim3(256), 0, st, part, parts,
                      ncols, dw, db, accumulate);
   MD2_LAUNCH_CHECK();

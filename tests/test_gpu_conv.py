@@ -53,6 +53,13 @@ CASES = [
     ((2, 32, 16, 52), 1, 3, 1, 1, True, "sigmoid", True),        # head4 geometry
     ((2, 128, 4, 13), 1, 3, 1, 1, True, "sigmoid", True),        # head2 (16 channel groups)
     ((12, 16, 128, 416), 1, 3, 1, 1, True, "sigmoid", True),     # head5 at bench size
+    # column-strip head kernels (W >= 64): ragged segments / bands / channel blocks, zero padding,
+    # both row folds inside one strip, the head3 geometry
+    ((2, 37, 13, 70), 1, 3, 1, 1, True, "sigmoid", True),
+    ((2, 7, 9, 66), 1, 3, 1, 1, False, None, True),
+    ((4, 8, 130, 256), 1, 3, 1, 1, False, None, True),           # zero padding, strip fwd/wgrad
+    ((1, 16, 4, 64), 1, 3, 1, 1, True, "sigmoid", True),
+    ((2, 64, 32, 104), 1, 3, 1, 1, True, "sigmoid", True),
 ]
 
 
@@ -71,15 +78,18 @@ def test_conv_fwd_bwd(case):
     from md2hip import ops
     xs, cout, k, stride, pad, reflect, act, has_bias = case
     g = torch.Generator().manual_seed(5)
-    x = torch.randn(*xs, generator=g, dtype=torch.float64)
-    w = torch.randn(cout, xs[1], k, k, generator=g, dtype=torch.float64) / (xs[1] * k * k) ** 0.5
-    b = torch.randn(cout, generator=g, dtype=torch.float64) if has_bias else None
+    # fp32-representable inputs: the fp64 reference sees exactly what the kernels see, so the
+    # tolerance measures the kernels' accumulation error alone (a cancelling bias-gradient sum
+    # would otherwise inherit the fp32 rounding of dy)
+    x = torch.randn(*xs, generator=g, dtype=torch.float64).float().double()
+    w = (torch.randn(cout, xs[1], k, k, generator=g, dtype=torch.float64) / (xs[1] * k * k) ** 0.5).float().double()
+    b = torch.randn(cout, generator=g, dtype=torch.float64).float().double() if has_bias else None
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     br = b.clone().requires_grad_(True) if has_bias else None
     pre = _ref_conv(xr, wr, br, stride, pad, reflect)
     y_ref = _ref_act(pre, act)
-    dy = torch.randn(pre.shape, generator=g, dtype=torch.float64)
+    dy = torch.randn(pre.shape, generator=g, dtype=torch.float64).float().double()
     pre.backward(dy)
 
     dev = torch.device("cuda")
