@@ -44,6 +44,14 @@ CASES = [
     ((6, 256, 4, 8), 512, 1, 2, 0, False, None, False),          # layer4 downsample
     ((2, 512, 2, 4), 256, 3, 1, 1, True, "elu", True),           # branch1.c1 reflect 2x4
     ((4, 512, 2, 4), 256, 3, 1, 1, False, "relu", True),         # pose conv1 on 2x4
+    # M <= 16 (16x16x4 MFMA kernel): Cout = 16 forward / Cin = 16 dgrad, reflect and zero padding,
+    # ragged pixel tiles, both block widths (BN 128 / 256), the bench-size branch-5 convs
+    ((2, 16, 24, 70), 16, 3, 1, 1, True, "elu", True),
+    ((2, 32, 12, 40), 16, 3, 1, 1, True, "elu", True),
+    ((3, 16, 9, 17), 16, 3, 1, 1, False, "relu", False),
+    ((2, 48, 5, 7), 8, 3, 1, 1, True, None, True),
+    ((12, 16, 128, 416), 16, 3, 1, 1, True, "elu", True),
+    ((12, 32, 64, 208), 16, 3, 1, 1, True, "elu", True),
     # Cout = 1 heads (VALU kernels of head.hip): reflect folds on 2/3-wide maps, zero padding,
     # ragged and > 8-channel groups, the bench-size full-resolution head
     ((2, 16, 2, 2), 1, 3, 1, 1, True, "sigmoid", True),          # every pixel folds twice
