@@ -76,7 +76,8 @@ struct PackJob {
   const float* w;
   PackDst f, d;        // forward (k over Cin, rows Cout) / dgrad (k over Cout, rows Cin)
   int Cout, Cin, KK;
-  long block_begin;    // first 256-element block of this job in the batched grid
+  int tiled;           // both operands tap-major k-contiguous, Cin, Cout % 16 == 0: LDS tiles
+  long block_begin;    // first block of this job in the batched grid
 };
 PackJob conv_pack_job(const ConvShape& s, const float* w, float* out_f, float* out_d);
 long conv_pack_job_blocks(const PackJob& j);

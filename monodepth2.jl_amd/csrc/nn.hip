@@ -176,26 +176,29 @@ int bn_apply(const BNApply& p, float* out, int N, int C, long HW, hipStream_t st
 
 
 // ---- fused finalise + apply.  A block covers 256 consecutive units (float4 or scalar), i.e. the
-// planes pl0..pl1 (plane = image*C + channel, <= 256 of them); thread t < #planes finalises the
-// channel of plane pl0+t from the partials in exactly bn_stats_final_kernel's order and
-// arithmetic (so mean/invstd are bit-identical to the two-kernel path), the scale/shift go
-// through LDS.  The block holding the first unit of image 0's plane of channel c writes mean[c],
+// planes pl0..pl1 (plane = image*C + channel, <= 256 of them); wave w finalises the channels of
+// planes pl0+w, pl0+w+4, ... from the partials (lane-parallel fixed-order sum + wave reduction,
+// same result in every block), the scale/shift go through LDS.  The block holding the first unit of image 0's plane of channel c writes mean[c],
 // invstd[c] and the running statistics.
+// called by a whole wave: lane l sums partials l, l+64, ... (fixed order), then a wave reduction
+// -- one partial-load latency per plane instead of `parts` dependent ones
 __device__ __forceinline__ void bn_finalise_plane(const BNStatsIn& s, int c, double total,
                                                   bool owner, float& sc, float& sh) {
   double a = 0.0, aa = 0.0;
   const double* q = s.part + (long)c * s.parts * 2;
-  for (int p = 0; p < s.parts; ++p) {
+  for (int p = threadIdx.x & 63; p < s.parts; p += 64) {
     a += q[2 * p];
     aa += q[2 * p + 1];
   }
+  a = wave_sum_d(a);
+  aa = wave_sum_d(aa);
   const double mu = a / total;
   const double var = fmax(aa / total - mu * mu, 0.0);
   const float meanf = (float)mu;
   const float isf = (float)(1.0 / sqrt(var + (double)s.eps));
   sc = s.gamma[c] * isf;
   sh = s.beta[c] - meanf * sc;
-  if (owner) {
+  if (owner && (threadIdx.x & 63) == 0) {
     s.mean[c] = meanf;
     s.invstd[c] = isf;
     if (s.run_mean) {
@@ -214,12 +217,20 @@ __global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNApplyFused p, flo
   const uint32_t u0 = blockIdx.x * 256u;
   const uint32_t pl0 = fdiv(u0, fdU);
   const uint32_t npl = fdiv(min(u0 + 255u, nu - 1u), fdU) - pl0 + 1u;
-  if (threadIdx.x < npl) {
-    const uint32_t pl = pl0 + threadIdx.x;
+  for (uint32_t t = threadIdx.x >> 6; t < npl; t += 4) {   // wave-uniform plane loop
+    const uint32_t pl = pl0 + t;
     const int c = (int)(pl - fdiv(pl, fdC) * fdC.d);
     const bool owner = pl < fdC.d && pl * fdU.d >= u0;
-    bn_finalise_plane(p.s1, c, total, owner, s_sc[threadIdx.x], s_sh[threadIdx.x]);
-    if (p.y2) bn_finalise_plane(p.s2, c, total, owner, s_sc2[threadIdx.x], s_sh2[threadIdx.x]);
+    float sc, sh;
+    bn_finalise_plane(p.s1, c, total, owner, sc, sh);
+    float sc2 = 0.f, sh2 = 0.f;
+    if (p.y2) bn_finalise_plane(p.s2, c, total, owner, sc2, sh2);
+    if ((threadIdx.x & 63) == 0) {
+      s_sc[t] = sc;
+      s_sh[t] = sh;
+      s_sc2[t] = sc2;
+      s_sh2[t] = sh2;
+    }
   }
   __syncthreads();
   const uint32_t u = u0 + threadIdx.x;
@@ -462,26 +473,30 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
   const uint32_t u0 = blockIdx.x * 256u;
   const uint32_t pl0 = fdiv(u0, fdU);
   const uint32_t npl = fdiv(min(u0 + 255u, nu - 1u), fdU) - pl0 + 1u;
-  if (threadIdx.x < npl) {
-    const uint32_t pl = pl0 + threadIdx.x;
+  for (uint32_t t = threadIdx.x >> 6; t < npl; t += 4) {   // one wave per plane (see bn_finalise_plane)
+    const uint32_t pl = pl0 + t;
     const int c = (int)(pl - fdiv(pl, fdC) * fdC.d);
     double sg = 0.0, sgx = 0.0;
     const double* q = part + (long)c * parts * 2;
-    for (int p = 0; p < parts; ++p) {
+    for (int p = threadIdx.x & 63; p < parts; p += 64) {
       sg += q[2 * p];
       sgx += q[2 * p + 1];
     }
-    const float dbf = (float)sg, dgf = (float)sgx;
-    if (pl < fdC.d && pl * fdU.d >= u0) {
-      dbeta[c] = dbf;
-      dgamma[c] = dgf;
+    sg = wave_sum_d(sg);
+    sgx = wave_sum_d(sgx);
+    if ((threadIdx.x & 63) == 0) {
+      const float dbf = (float)sg, dgf = (float)sgx;
+      if (pl < fdC.d && pl * fdU.d >= u0) {
+        dbeta[c] = dbf;
+        dgamma[c] = dgf;
+      }
+      const float is = invstd[c];
+      s_k0[t] = gamma[c] * is;
+      s_db[t] = dbf * invL;
+      s_dg[t] = dgf * invL;
+      s_mu[t] = mean[c];
+      s_is[t] = is;
     }
-    const float is = invstd[c];
-    s_k0[threadIdx.x] = gamma[c] * is;
-    s_db[threadIdx.x] = dbf * invL;
-    s_dg[threadIdx.x] = dgf * invL;
-    s_mu[threadIdx.x] = mean[c];
-    s_is[threadIdx.x] = is;
   }
   __syncthreads();
   const uint32_t u = u0 + threadIdx.x;
