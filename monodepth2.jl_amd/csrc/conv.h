@@ -94,10 +94,18 @@ int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const 
 int conv_dgrad(const ConvShape& s, const float* dy, const float* wpacked_d, const TensorOut& dx,
                ConvWorkspace ws, hipStream_t st);
 // dW [Cout][Cin*KH*KW] (store or accumulate) and optional db [Cout]
+// db_part/db_parts: bias-gradient partials [Cout][db_parts] already summed by act_backward_bias
+// (the bias partial pass over dY is then skipped)
 int conv_wgrad(const ConvShape& s, const TensorIn& x, const float* dy, float* dw, float* db,
-               int accumulate, ConvWorkspace ws, hipStream_t st);
+               int accumulate, ConvWorkspace ws, hipStream_t st, const float* db_part = nullptr,
+               int db_parts = 0);
 
 // dPre = dOut * act'(out) (act from the stored post-activation output), elementwise
 int act_backward(const float* out, const float* dout, float* dpre, long n, int act, hipStream_t st);
+// the same over [N][C][HW] planes fused with the per-channel partial sums of dPre (the bias
+// gradient of the conv that produced `out`): part [C][parts], parts = act_bias_parts(C, N, HW)
+int act_bias_parts(int C, int N, long HW);
+int act_backward_bias(const float* out, const float* dout, float* dpre, int N, int C, long HW,
+                      int act, float* part, hipStream_t st);
 
 }  // namespace md2

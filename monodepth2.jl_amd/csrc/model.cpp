@@ -463,6 +463,7 @@ class Model {
       cws.ptr = q;
       cws.bytes = wsn + 256;
     }
+    MD2_TRY(alloc(&bp_ws, BP_WS));
     {
       double* q;
       void* v;
@@ -766,7 +767,9 @@ class Model {
     ConvShape s = c.s;
     s.N = nimg;
     hipEvent_t e = prof_begin(st);
-    MD2_TRY(conv_wgrad(s, in, dy, grads + c.p.w, Gd(c.p.b), 0, cws, st));
+    MD2_TRY(conv_wgrad(s, in, dy, grads + c.p.w, Gd(c.p.b), 0, cws, st, c.p.b >= 0 ? bp_pending : nullptr,
+                       bp_parts));
+    bp_pending = nullptr;
     prof_end(e, c.cat, conv_flops(s), st);
     return MD2_OK;
   }
@@ -794,6 +797,24 @@ class Model {
     prof_end(e, c.cat, conv_flops(s), st);
     return MD2_OK;
   }
+  // activation pullback fused with the bias-gradient partials of the conv that produced `out`
+  // (consumed by that conv's next conv_w)
+  float* bp_ws = nullptr;
+  const float* bp_pending = nullptr;
+  int bp_parts = 0;
+  int act_bias(const float* out, const float* dout, float* dpre, int nimg, int C, long HW, int act,
+               hipStream_t st) {
+    if (HW % 4 != 0 || (long)C * act_bias_parts(C, nimg, HW) > BP_WS) {
+      bp_pending = nullptr;
+      return act_backward(out, dout, dpre, (long)nimg * C * HW, act, st);
+    }
+    MD2_TRY(act_backward_bias(out, dout, dpre, nimg, C, HW, act, bp_ws, st));
+    bp_pending = bp_ws;
+    bp_parts = act_bias_parts(C, nimg, HW);
+    return MD2_OK;
+  }
+  static constexpr long BP_WS = 8192;
+
   int bn_bwd(RBN& bn, const float* dout, const float* mask, const float* y, int nimg, long HW,
              float* dy, float* dres, int dres_acc, hipStream_t st) {
     BNStatsWs w = bnws;
@@ -835,15 +856,15 @@ class Model {
     // ---- PoseDecoder backward
     MD2_TRY(pose_head_bwd(d_pose, 2 * N, 256, hw4, P(spec.p3.w), means, DPRE, Gd(spec.p3.w),
                           Gd(spec.p3.b), st));
-    MD2_TRY(act_backward(pc2, DPRE, DPRE, 2L * N * 256 * hw4, ACT_RELU, st));
+    MD2_TRY(act_bias(pc2, DPRE, DPRE, 2 * N, 256, hw4, ACT_RELU, st));
     MD2_TRY(conv_wd(p2, 2 * N, tin(pc1, 256, hw4), DPRE, d_pc1, 256 * hw4, 0, st));
-    MD2_TRY(act_backward(pc1, d_pc1, d_pc1, 2L * N * 256 * hw4, ACT_RELU, st));
+    MD2_TRY(act_bias(pc1, d_pc1, d_pc1, 2 * N, 256, hw4, ACT_RELU, st));
     TensorIn pin = tin(sqo, 256, hw4);
     pin.p1 = sqo + (long)N * 256 * hw4;
     pin.bs1 = 256 * hw4;
     MD2_TRY(conv_wd(p1, 2 * N, pin, d_pc1, d_pin, 512 * hw4, 0, st));
     MD2_TRY(pair_grad_gather(d_pin, N, 256, hw4, d_sq, st));
-    MD2_TRY(act_backward(sqo, d_sq, d_sq, (long)B * 256 * hw4, ACT_RELU, st));
+    MD2_TRY(act_bias(sqo, d_sq, d_sq, B, 256, hw4, ACT_RELU, st));
     float* d_f4 = stages[3].back().d_out;
     MD2_TRY(conv_wd(sq, B, tin(feat[4], featC[4], hw4), d_sq, d_f4, (long)featC[4] * hw4, 0, st));
     // ---- DepthDecoder backward (reverse branch order)
@@ -855,7 +876,7 @@ class Model {
       if (d.head >= 0) {
         MD2_TRY(conv_wd(d.hc, N, tin(d.o2, co, hw2), d.d_head, d.d_o2, co * hw2, i < nb - 1 ? 1 : 0, st));
       }
-      MD2_TRY(act_backward(d.o2, d.d_o2, DPRE, (long)N * co * hw2, ACT_ELU, st));
+      MD2_TRY(act_bias(d.o2, d.d_o2, DPRE, N, co, hw2, ACT_ELU, st));
       TensorIn in = tin(d.up, co, hw2);
       float* dskip = nullptr;
       long skip_bs = 0;
@@ -868,7 +889,7 @@ class Model {
       }
       MD2_TRY(conv_wd(d.c2, N, in, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
       MD2_TRY(upsample2_bwd(DUP, N, co, d.h, d.w, DO1, st));
-      MD2_TRY(act_backward(d.o1, DO1, DO1, (long)N * co * hw, ACT_ELU, st));
+      MD2_TRY(act_bias(d.o1, DO1, DO1, N, co, hw, ACT_ELU, st));
       const float* xin;
       int cin;
       float* dx;
