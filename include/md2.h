@@ -80,6 +80,8 @@ typedef struct md2_loss_out {
   float* d_pose;                     /* [2n][6] d loss / d (rvec, tvec)                       */
   float* vis_loss;                   /* [nscales][n][h][w] per-pixel warp loss (vis_loss)     */
   signed char* vis_sel;              /* [nscales][n][h][w] argmin source (-1 = automask)      */
+  float* vis_warped;                 /* [2][n][c][h][w] both sources warped by the LAST scale
+                                        (train_loss vis_warped, src/training.jl:71-73)        */
 } md2_loss_out;
 
 /* disp[s]: [n][scale_h][scale_w]; pose: [2n][6] = (rvec, tvec) for (source s, sample i) at row

@@ -82,6 +82,7 @@ int md2_loss_fwd_bwd(const md2_loss_cfg* cfg, const float* const* disp, const fl
   o.d_pose = out->d_pose;
   o.vis_loss = out->vis_loss;
   o.vis_sel = out->vis_sel;
+  o.vis_warped = out->vis_warped;
   return loss_tail_run(to_tail_cfg(cfg), disp, pose, x, automask, dloss, o, workspace,
                        (hipStream_t)stream);
 }

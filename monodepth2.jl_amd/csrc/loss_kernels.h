@@ -78,6 +78,8 @@ struct FinalizeArgs {
 };
 
 int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st);
+// warped sources only (train_loss vis_warped): out [2][N][C][H][W]
+int launch_warp_vis(const PhotoArgs& a, const Geom& g, int C, float* out, hipStream_t st);
 long photometric_blocks(int W, int H, int N);
 long smooth_blocks(int W, int H, int N);
 int launch_disp_sum(const float* disp, int dw, int dh, float rx, float ry, int W, int H, int N,

@@ -890,6 +890,56 @@ int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st)
   return MD2_OK;
 }
 
+// Visualisation warp (train_loss vis_warped, src/training.jl:48-57,71-73): both sources
+// resampled through the scale's depth and pose, no loss, no backward.  One thread per target
+// pixel, all C channels of both sources; same geometry helpers as the photometric kernel.
+template <int C>
+__global__ __launch_bounds__(256) void warp_vis_kernel(PhotoArgs a, Geom g, float* __restrict__ out) {
+  const int HW = g.W * g.H;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)a.N * HW) return;
+  const int n = (int)(idx / HW), pix = (int)(idx - (long)n * HW);
+  const int Y = pix / g.W, X = pix - Y * g.W;
+  const float d = disp_at(a.disp + (long)n * a.dw * a.dh, a.dw, a.dh, a.rx, a.ry, g.W, g.H, X, Y);
+  const float depth = 1.f / (d * g.disp_range + g.min_disp);
+  float r0, r1, r2;
+  ray_at(g, X, Y, r0, r1, r2);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    Proj p;
+    project_point(g, a.Rt + ((long)s * a.N + n) * 12, depth, r0, r1, r2, p);
+    const float x = fminf(fmaxf(p.ix, 0.f), (float)(g.W - 1));
+    const float y = fminf(fmaxf(p.iy, 0.f), (float)(g.H - 1));
+    const int x0 = (int)x, y0 = (int)y;
+    const int x1 = min(x0 + 1, g.W - 1), y1 = min(y0 + 1, g.H - 1);
+    const float fx = x - (float)x0, fy = y - (float)y0;
+    const float* src = a.x + (long)n * a.x_sample_stride + (long)(s ? a.src1 : a.src0) * a.x_frame_stride;
+    float* o = out + ((long)s * a.N + n) * C * HW + pix;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float* q = src + (long)c * HW;
+      const float v = (1.f - fy) * ((1.f - fx) * q[y0 * g.W + x0] + fx * q[y0 * g.W + x1]) +
+                      fy * ((1.f - fx) * q[y1 * g.W + x0] + fx * q[y1 * g.W + x1]);
+      o[(long)c * HW] = v;
+    }
+  }
+}
+
+int launch_warp_vis(const PhotoArgs& a, const Geom& g, int C, float* out, hipStream_t st) {
+  const long n = (long)a.N * g.W * g.H;
+  const dim3 grid((unsigned)cdiv(n, 256L));
+  if (C == 3)
+    hipLaunchKernelGGL(warp_vis_kernel<3>, grid, dim3(256), 0, st, a, g, out);
+  else if (C == 1)
+    hipLaunchKernelGGL(warp_vis_kernel<1>, grid, dim3(256), 0, st, a, g, out);
+  else {
+    set_error("warp_vis: channels must be 1 or 3");
+    return MD2_ENOTSUP;
+  }
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 long photometric_blocks(int W, int H, int N) { return (long)cdiv(W, PT_W) * cdiv(H, PT_H) * N; }
 long smooth_blocks(int W, int H, int N) { return (long)cdiv(W, SM_W) * cdiv(H, SM_H) * N; }
 

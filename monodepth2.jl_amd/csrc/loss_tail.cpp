@@ -112,6 +112,7 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[2 * s], st));
     MD2_TRY(launch_photometric(pa, g, c.C, st));
     if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[2 * s + 1], st));
+    if (o.vis_warped && s == c.nscales - 1) MD2_TRY(launch_warp_vis(pa, g, c.C, o.vis_warped, st));
 
     SmoothArgs sa{};
     sa.disp = disp[s];

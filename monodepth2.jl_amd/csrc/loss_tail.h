@@ -31,6 +31,7 @@ struct LossTailOut {
   float* d_pose;
   float* vis_loss;
   signed char* vis_sel;
+  float* vis_warped;                    // [2][N][C][H][W] warped sources at the last scale or nullptr
   hipEvent_t* photo_events = nullptr;   // optional [2*nscales] around each photometric launch
 };
 

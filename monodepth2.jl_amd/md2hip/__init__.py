@@ -9,8 +9,9 @@ from .loss import Params, TrainCache, depth10k_intrinsics, loss_tail, pack_poses
 from .model import (ADAM, DepthDecoder, Model, Pose, PoseDecoder, ResidualNetwork, ResNet,  # noqa: F401
                     eval_disparity, gradient, param_table, train_loss, train_step)
 from .slow_depth import SlowDepth, adam_update, slow_depth  # noqa: F401
+from .checkpoint import load_checkpoint, save_checkpoint  # noqa: F401
 
 __all__ = ["Params", "TrainCache", "depth10k_intrinsics", "loss_tail", "pack_poses", "lib", "MD2Error",
            "ADAM", "DepthDecoder", "Model", "Pose", "PoseDecoder", "ResidualNetwork", "ResNet",
            "eval_disparity", "gradient", "param_table", "train_loss", "train_step",
-           "SlowDepth", "adam_update", "slow_depth"]
+           "SlowDepth", "adam_update", "slow_depth", "load_checkpoint", "save_checkpoint"]

@@ -34,7 +34,7 @@ class LossOut(C.Structure):
     _fields_ = [
         ("loss", C.c_void_p), ("terms", C.c_void_p),
         ("d_disp", C.c_void_p * MAX_SCALES), ("d_pose", C.c_void_p),
-        ("vis_loss", C.c_void_p), ("vis_sel", C.c_void_p),
+        ("vis_loss", C.c_void_p), ("vis_sel", C.c_void_p), ("vis_warped", C.c_void_p),
     ]
 
 

@@ -90,7 +90,8 @@ def loss_tail(disparities, poses, x, auto_loss, cache: TrainCache, params: Param
     disparities: list of [N,1,h,w] float32 CUDA tensors (one per scale); poses: list of
     (rvec [N,3], tvec [N,3]) per source; x: [N,L,C,H,W]; auto_loss: [N,1,H,W] or None.
     Returns a dict: loss [1], terms [nscales,2], d_disp (list), d_pose [2N,6] and, with
-    ``visualize``, vis_loss / vis_sel [nscales,N,H,W] (training.jl:71-74 vis_loss)."""
+    ``visualize``, vis_loss / vis_sel [nscales,N,H,W] (training.jl:71-74 vis_loss) and
+    vis_warped [2,N,C,H,W] (both sources warped by the last scale, training.jl:71-73)."""
     import torch
     N, L, C_, H, W = x.shape
     dev = x.device
@@ -111,6 +112,7 @@ def loss_tail(disparities, poses, x, auto_loss, cache: TrainCache, params: Param
     if visualize:
         res["vis_loss"] = torch.empty(len(disparities), N, H, W, dtype=torch.float32, device=dev)
         res["vis_sel"] = torch.empty(len(disparities), N, H, W, dtype=torch.int8, device=dev)
+        res["vis_warped"] = torch.empty(2, N, C_, H, W, dtype=torch.float32, device=dev)
     am = None
     if params.automasking:
         if auto_loss is None:
@@ -124,6 +126,7 @@ def loss_tail(disparities, poses, x, auto_loss, cache: TrainCache, params: Param
     out.d_pose = None if res["d_pose"] is None else res["d_pose"].data_ptr()
     out.vis_loss = res["vis_loss"].data_ptr() if visualize else None
     out.vis_sel = res["vis_sel"].data_ptr() if visualize else None
+    out.vis_warped = res["vis_warped"].data_ptr() if visualize else None
     disp_arr = ptr_array(disparities)
     check(lib().md2_loss_fwd_bwd(C.byref(cfg), C.cast(disp_arr, _lib.FP), ptr(pose), ptr(x), ptr(am),
                                  C.c_float(dloss), C.byref(out), ptr(ws), stream_of(dev)),

@@ -20,7 +20,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import ModelCfg, check, lib, ptr, stream_of
-from .loss import Params, TrainCache, depth10k_intrinsics
+from .loss import Params, TrainCache, depth10k_intrinsics, loss_tail
 
 
 class ResidualNetwork:
@@ -291,10 +291,18 @@ def train_loss(model: Model, x, auto_loss, cache: TrainCache, params: Params,
     the backward.  Returns (loss, vis_disparity, vis_warped, vis_loss)."""
     ex = model.executor(tuple(x.shape), cache, params)
     loss = ex.forward_loss(x, auto_loss)
-    vis_disparity = None
-    if do_visualization:
-        vis_disparity = ex.outputs()[0][-1].cpu()
-    return loss, vis_disparity, None, None
+    if not do_visualization:
+        return loss, None, None, None
+    # training.jl:34-37,71-74: the last disparity, both warped sources and the per-pixel warp
+    # loss of the last scale, on the host.  Recomputed from the model outputs by the loss-tail
+    # kernels (forward only, after the step's own forward; the gradient state is untouched).
+    disps, pose = ex.outputs()
+    N = x.shape[0]
+    poses = [(pose[s * N:(s + 1) * N, 0:3], pose[s * N:(s + 1) * N, 3:6]) for s in range(2)]
+    vis = loss_tail(disps, poses, x.contiguous(), auto_loss, cache, params, grads=False,
+                    visualize=True)
+    return (loss, disps[-1].cpu(), [w.cpu() for w in vis["vis_warped"].unbind(0)],
+            vis["vis_loss"][-1].unsqueeze(1).cpu())
 
 
 def gradient(model: Model):

@@ -136,3 +136,25 @@ def test_so3_compose_roundtrip():
         got = Rt[s * N:(s + 1) * N].cpu().double()
         assert torch.allclose(got[:, :9].view(N, 3, 3), R, atol=1e-6)
         assert torch.allclose(got[:, 9:], tt, atol=1e-6)
+
+
+@pytest.mark.parametrize("N,C,H,W", [(2, 3, 32, 64), (2, 1, 32, 64), (1, 3, 128, 416)])
+def test_loss_tail_vis_outputs(N, C, H, W):
+    """train_loss visualisation outputs (src/training.jl:71-74): both sources warped by the last
+    scale against the oracle's ``warp`` (fp32 vs fp64 on kink-free ramp sources: rel 1e-5), and
+    the last scale's per-pixel warp-loss map whose mean is that scale's warp term."""
+    x = D.triplets(N, C, H, W, seed=5, ramp_sources=True)
+    K, invK = D.intrinsics(W, H)
+    disps = D.disparities(N, H, W, seed=9)
+    poses = D.poses(N, seed=15)
+    g = _gpu(disps, poses, x, K, invK, None)
+    assert g["vis_warped"].shape == (2, N, C, H, W)
+    d = disps[-1]
+    if d.shape[-2:] != (H, W):
+        d = O.upsample_bilinear_size(d, (H, W))
+    Ps = O.poses_to_transforms(poses, (1, 3), 2)
+    ref = O.warp(d, x, Ps, K, invK, (1, 3), 0.1, 100.0)
+    for s in range(2):
+        assert D.rel_err(g["vis_warped"][s], ref[s]) < 1e-5, s
+    vl = g["vis_loss"][-1]
+    assert abs(vl.double().mean().item() - g["terms"][-1, 0].item()) <= 1e-5 * abs(g["terms"][-1, 0].item())

@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 import torch
 
+from oracle import md2_oracle as O
 from tests import _data as D
 
 pytestmark = pytest.mark.gpu
@@ -155,3 +156,35 @@ def test_encoder_layers_parity(arch):
     errs["pose.conv2"] = D.rel_err(t["pose.conv2"], F.relu(F.conv2d(t["pose.conv1"], P["pose.conv2.weight"], P["pose.conv2.bias"], padding=1)))
     bad = {k: v for k, v in errs.items() if v > 1e-5}
     assert not bad, bad
+
+
+def test_train_loss_visualization():
+    """train_loss(..., do_visualization=true) returns (loss, vis_disparity, vis_warped, vis_loss)
+    (src/training.jl:34-37,71-74); the warped sources match the oracle's warp of the model's own
+    last disparity and poses."""
+    import md2hip
+    N, H, W = 2, 64, 128
+    enc = md2hip.ResNet(18, in_channels=3)
+    model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
+                                                  embedding_levels=0), md2hip.PoseDecoder(512), seed=42)
+    K, invK = md2hip.depth10k_intrinsics(W, H)
+    cache = md2hip.TrainCache(K=K, invK=invK)
+    params = md2hip.Params(target_size=(W, H), batch_size=N, automasking=False)
+    x = D.triplets(N, 3, H, W, seed=3, ramp_sources=True).float().cuda().contiguous()
+    loss, vd, vw, vl = md2hip.train_loss(model, x, None, cache, params, True)
+    torch.cuda.synchronize()
+    assert vd.shape == (N, 1, H, W) and vl.shape == (N, 1, H, W) and len(vw) == 2
+    assert all(w.shape == (N, 3, H, W) for w in vw)
+    assert torch.isfinite(vl).all() and (vl >= 0).all()
+    disps, pose = model._last.outputs()
+    pose = pose.cpu().double()
+    poses = [(pose[s * N:(s + 1) * N, 0:3], pose[s * N:(s + 1) * N, 3:6]) for s in range(2)]
+    Ps = O.poses_to_transforms(poses, (1, 3), 2)
+    ref = O.warp(vd.double(), x.cpu().double(), Ps, torch.tensor(K, dtype=torch.float64),
+                 torch.tensor(invK, dtype=torch.float64), (1, 3), 0.1, 100.0)
+    for s in range(2):
+        assert D.rel_err(vw[s], ref[s]) < 1e-5, s
+    # the gradient path still works after a visualising train_loss
+    md2hip.gradient(model)
+    torch.cuda.synchronize()
+    assert torch.isfinite(model.grad).all()
