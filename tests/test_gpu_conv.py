@@ -52,6 +52,11 @@ CASES = [
     ((2, 48, 5, 7), 8, 3, 1, 1, True, None, True),
     ((12, 16, 128, 416), 16, 3, 1, 1, True, "elu", True),
     ((12, 32, 64, 208), 16, 3, 1, 1, True, "elu", True),
+    # Cout <= 16 wgrad (conv_wgrad16_kernel: 16-channel groups, K split over waves and slabs)
+    ((5, 64, 33, 47), 16, 3, 1, 1, False, None, True),           # 4 channel groups, ragged K
+    ((1, 16, 3, 5), 12, 3, 1, 1, True, "elu", True),             # K < one 64-pixel chunk
+    ((3, 32, 10, 30), 20, 3, 1, 1, False, "relu", True),         # Cout 20: ragged second row tile
+    ((12, 96, 64, 208), 32, 3, 1, 1, True, "elu", True),         # decoder level-4 conv2 at bench size
     # Cout = 1 heads (VALU kernels of head.hip): reflect folds on 2/3-wide maps, zero padding,
     # ragged and > 8-channel groups, the bench-size full-resolution head
     ((2, 16, 2, 2), 1, 3, 1, 1, True, "sigmoid", True),          # every pixel folds twice
