@@ -135,6 +135,18 @@ int md2_upsample2_fwd(const float* x, int n, int c, int h, int w, float* y, void
 int md2_upsample2_bwd(const float* dy, int n, int c, int h, int w, float* dx, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * MPI mode (src/model.jl:1-55; forward only upstream).  md2_mpi_embed_features
+ * builds the DepthDecoder input of one feature level: out [n*num_bins][c + 2L+1][h][w] with
+ * image b*num_bins + p = cat(feat[b], repeat(embed(bins[b][p]), h, w)); embed(x) = [x, sin(2^i x),
+ * cos(2^i x) for i in 0:L-1] (src/model.jl:4-15); feat[b] at feat + b*sample_stride.
+ * md2_concat_channels: cat(a, b; dims=3) for [n][ca][hw] and [n][cb][hw] (BranchBlock skip).
+ * ---------------------------------------------------------------------------------------- */
+int md2_mpi_embed_features(const float* feat, long long sample_stride, int n, int c, int h, int w,
+                           const float* bins, int num_bins, int L, float* out, void* stream);
+int md2_concat_channels(const float* a, int ca, const float* b, int cb, int n, long long hw,
+                        float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Model: Model(ResidualNetwork(arch), DepthDecoder(embedding_levels=0), PoseDecoder) in mono
  * mode (src/model.jl:24-70), train_loss (src/training.jl:21-78), its pullback, Flux ADAM.
  * Parameters / gradients are CALLER-owned flat fp32 device vectors; their order is the table
@@ -191,6 +203,9 @@ int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, f
                          float* adam_v, float lr, int step, float* loss, void* stream);
 /* device pointers of the last forward: disparities per level and poses [2*batch][6] */
 int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose);
+/* The five encoder stage outputs of the last forward (device memory owned by the model):
+ * feat[k] = [3n frame-major images][c[k]][h[k]][w[k]] (image l*n + i = frame l of sample i). */
+int md2_model_features(md2_model* m, const float** feat, int* c, int* h, int* w);
 /* HIP-event profiling of the hot kernels on the model's stream (bench roofline): categories
  * 0 = zero-padded 3x3 convs (encoder + pose decoder; fwd/dgrad/wgrad incl. their split-K
  * reductions, work = algorithmic FLOP), 1 = other convs,

@@ -204,6 +204,18 @@ int md2_upsample2_fwd(const float* x, int n, int c, int h, int w, float* y, void
   MD2_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0, "upsample2_fwd args");
   return upsample2_fwd(x, n, c, h, w, y, (hipStream_t)stream);
 }
+int md2_mpi_embed_features(const float* feat, long long sample_stride, int n, int c, int h, int w,
+                           const float* bins, int num_bins, int L, float* out, void* stream) {
+  MD2_CHECK_ARG(feat && bins && out && n > 0 && c > 0 && h > 0 && w > 0 && num_bins > 0 && L >= 0 &&
+                    sample_stride >= (long long)c * h * w, "mpi_embed_features args");
+  return mpi_embed_features(feat, (long)sample_stride, n, c, h, w, bins, num_bins, L, out,
+                            (hipStream_t)stream);
+}
+int md2_concat_channels(const float* a, int ca, const float* b, int cb, int n, long long hw,
+                        float* out, void* stream) {
+  MD2_CHECK_ARG(a && b && out && ca > 0 && cb > 0 && n > 0 && hw > 0, "concat_channels args");
+  return concat_channels(a, ca, b, cb, n, (long)hw, out, (hipStream_t)stream);
+}
 int md2_upsample2_bwd(const float* dy, int n, int c, int h, int w, float* dx, void* stream) {
   MD2_CHECK_ARG(dy && dx && n > 0 && c > 0 && h > 0 && w > 0, "upsample2_bwd args");
   return upsample2_bwd(dy, n, c, h, w, dx, (hipStream_t)stream);
@@ -336,6 +348,11 @@ int md2_model_profile_read(md2_model* m, double* out, int ncat) {
 int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose) {
   MD2_CHECK_ARG(m, "model");
   return model_outputs(m->impl, disp, w, h, pose);
+}
+
+int md2_model_features(md2_model* m, const float** feat, int* c, int* h, int* w) {
+  MD2_CHECK_ARG(m && feat && c && h && w, "model_features args");
+  return model_features(m->impl, feat, c, h, w);
 }
 
 int md2_model_debug_tensor(md2_model* m, int index, const char** name, const void** ptr,

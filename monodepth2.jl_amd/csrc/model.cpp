@@ -1080,6 +1080,17 @@ int model_outputs(Model* m, const float** disp, int* dw, int* dh, const float** 
   return MD2_OK;
 }
 
+int model_features(Model* m, const float** feat, int* c, int* h, int* w) {
+  MD2_CHECK_ARG(m, "model");
+  for (int k = 0; k < 5; ++k) {
+    feat[k] = m->feat[k];
+    c[k] = m->featC[k];
+    h[k] = m->featH[k];
+    w[k] = m->featW[k];
+  }
+  return MD2_OK;
+}
+
 int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipStream_t st) {
   MD2_CHECK_ARG(m && x && n >= 1 && n <= m->N, "eval_disparity: 1 <= n <= batch");
   TensorIn in = Model::tin(x, m->cfg.arch.in_ch, (long)m->cfg.H * m->cfg.W);

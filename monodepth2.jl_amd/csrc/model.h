@@ -61,6 +61,8 @@ int model_adam(Model* m, float* adam_m, float* adam_v, float lr, float b1, float
 int model_repack(Model* m, hipStream_t st);   // after the parameters changed
 // outputs of the last forward
 int model_outputs(Model* m, const float** disp, int* dw, int* dh, const float** pose);
+// the five encoder stage outputs of the last forward: [3N frame-major images][c][h][w]
+int model_features(Model* m, const float** feat, int* c, int* h, int* w);
 // inference: eval_disparity (src/model.jl:63) on x [n][C][H][W], n <= N*3
 int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipStream_t st);
 int model_debug_tensor(Model* m, int index, const char** name, const void** ptr, int* dims);

@@ -71,6 +71,13 @@ int maxpool_bwd(const float* dy, const unsigned char* arg, int N, int C, int H, 
 // ---- upsample_bilinear(x, (2,2)), align_corners = true ----
 int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStream_t st);
 int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStream_t st);
+// MPI-mode decoder input (src/model.jl:39-50): out[(b*P + p)][0:C] = feat[b], out[..][C + e] =
+// embed(bins[b][p])[e] broadcast over h x w (e < 2L+1: x, sin(2^i x), cos(2^i x))
+int mpi_embed_features(const float* feat, long sample_stride, int N, int C, int h, int w,
+                       const float* bins, int P, int L, float* out, hipStream_t st);
+// channel concatenation cat(a, b; dims=3) of [N][ca][hw] and [N][cb][hw]
+int concat_channels(const float* a, int ca, const float* b, int cb, int N, long hw, float* out,
+                    hipStream_t st);
 
 // ---- pose head: pose[q][k] = 0.01 * (b[k] + sum_c W[k][c] * mean_hw(x[q][c])) ----
 int pose_head_fwd(const float* x, int Q, int C, long HW, const float* w, const float* b,

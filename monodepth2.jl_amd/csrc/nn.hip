@@ -753,6 +753,66 @@ __global__ __launch_bounds__(256) void upsample2_bwd_kernel(const float* __restr
   dx[i] = s;
 }
 
+// MPI-mode decoder input: repeat(target features, planes) ++ repeat(embed(bins), h, w) along
+// channels, planes merged into the batch (src/model.jl:39-50, embed :4-15).  One thread per
+// output element; the embedding channel is recomputed per element (2 transcendental ops at most).
+__global__ __launch_bounds__(256) void mpi_embed_kernel(const float* __restrict__ feat, long sstride,
+                                                        int C, int hw, const float* __restrict__ bins,
+                                                        int P, int E, float* __restrict__ out, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int CE = C + E;
+  const int px = (int)(i % hw);
+  const long t = i / hw;
+  const int c = (int)(t % CE);
+  const long img = t / CE;              // b * P + p
+  const int b = (int)(img / P), p = (int)(img - (long)b * P);
+  float v;
+  if (c < C) {
+    v = feat[(long)b * sstride + (long)c * hw + px];
+  } else {
+    const int e = c - C;
+    const float x = bins[(long)b * P + p];
+    if (e == 0) {
+      v = x;
+    } else {
+      const float a = ldexpf(x, (e - 1) >> 1);  // 2^i x, exact in fp32 like the reference's 2^i .* x
+      v = (e & 1) ? sinf(a) : cosf(a);
+    }
+  }
+  out[i] = v;
+}
+
+int mpi_embed_features(const float* feat, long sample_stride, int N, int C, int h, int w,
+                       const float* bins, int P, int L, float* out, hipStream_t st) {
+  const long n = (long)N * P * (C + 2 * L + 1) * h * w;
+  MD2_TRY(check_u31(n));
+  hipLaunchKernelGGL(mpi_embed_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, feat, sample_stride, C,
+                     h * w, bins, P, 2 * L + 1, out, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+__global__ __launch_bounds__(256) void concat_kernel(const float* __restrict__ a, int ca,
+                                                     const float* __restrict__ b, int cb, long hw,
+                                                     float* __restrict__ out, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long px = i % hw, t = i / hw;
+  const int c = (int)(t % (ca + cb));
+  const long img = t / (ca + cb);
+  out[i] = c < ca ? a[(img * ca + c) * hw + px] : b[(img * cb + (c - ca)) * hw + px];
+}
+
+int concat_channels(const float* a, int ca, const float* b, int cb, int N, long hw, float* out,
+                    hipStream_t st) {
+  const long n = (long)N * (ca + cb) * hw;
+  MD2_TRY(check_u31(n));
+  hipLaunchKernelGGL(concat_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, a, ca, b, cb, hw, out, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 static inline float up_ratio(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
 
 int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStream_t st) {

@@ -100,6 +100,11 @@ _SIGS = {
     "md2_model_eval_disparity": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_void_p), P]),
     "md2_model_debug_tensor": (C.c_int, [P, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_void_p),
                                          C.POINTER(C.c_int)]),
+    "md2_model_features": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                     C.POINTER(C.c_int)]),
+    "md2_mpi_embed_features": (C.c_int, [P, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int,
+                                         C.c_int, P, P]),
+    "md2_concat_channels": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_longlong, P, P]),
     "md2_model_set_profiling": (C.c_int, [P, C.c_int]),
     "md2_model_profile_read": (C.c_int, [P, C.POINTER(C.c_double), C.c_int]),
 }

@@ -49,7 +49,8 @@ class DepthDecoder:
             raise ValueError("`scale_levels` should be at most of length 5 and have values in [1, 5] range.")
         if embedding_levels != 0:
             # defects D2/D4: the MPI-embedding decoder is forward-only upstream
-            raise NotImplementedError("the HIP train step runs the mono DepthDecoder (embedding_levels=0)")
+            raise NotImplementedError("the HIP train step runs the mono DepthDecoder (embedding_levels=0); "
+                                      "MPI mode (forward only, as upstream): md2hip.MPIDepthDecoder + md2hip.mpi_forward")
         if levels != sorted(set(levels)) or levels[-1] != 5 or levels[0] < 2:
             raise NotImplementedError("HIP DepthDecoder supports increasing scale_levels in 2:5 ending at 5")
         self.encoder_channels = tuple(encoder_channels)

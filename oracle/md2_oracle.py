@@ -559,6 +559,27 @@ def disparity_bins(num_bins: int, u: torch.Tensor, near=1.0, far=0.001):
     return edges.unsqueeze(0) + u * interval
 
 
+def mpi_model_forward(P, x, u, source_ids=(1, 3), target_id=2, arch=18, scale_levels=(2, 3, 4, 5),
+                      embedding_levels=21):
+    """MPI-mode ``(m::Model)(x, source_ids, target_id; num_bins)`` disparities -- src/model.jl:31-55
+    with the bin draw injected (``u`` [N, num_bins]).  P holds the encoder and the
+    ``DepthDecoder(; embedding_levels)`` parameters.  Returns disparities [N*num_bins,1,h,w] per
+    scale, image b*num_bins + p (planes merged into the batch, model.jl:48-49)."""
+    N, L, C, H, W = x.shape
+    nb = u.shape[1]
+    feats = resnet_stages(P, x.reshape(N * L, C, H, W), arch)
+    bins = disparity_bins(nb, u.to(x.dtype))
+    emb = embed(bins, (embedding_levels - 1) // 2)                  # [N, nb, E]
+    levels = []
+    for f in feats:
+        f = f.reshape(N, L, *f.shape[1:])[:, target_id - 1]          # [N, c, h, w]
+        c, h, w = f.shape[1:]
+        rep = f.unsqueeze(1).expand(N, nb, c, h, w)
+        e = emb[:, :, :, None, None].expand(N, nb, emb.shape[-1], h, w)
+        levels.append(torch.cat([rep, e], 2).reshape(N * nb, c + emb.shape[-1], h, w))
+    return depth_decoder(P, levels, scale_levels)
+
+
 # ----------------------------------------------------------------------------------------------
 # Optimiser -- Flux ADAM (scripts/script.jl:85, src/simple_depth.jl:16)
 # ----------------------------------------------------------------------------------------------
