@@ -813,6 +813,44 @@ int concat_channels(const float* a, int ca, const float* b, int cb, int N, long 
   return MD2_OK;
 }
 
+// Tiled adjoint: a 32 x 8 block of input pixels of one plane stages the (2*8+4) x (2*32+4)
+// output-gradient window it reads in LDS (coalesced rows, each element fetched once instead of
+// up to 16 times through the cache), then every thread contracts its 6 x 6 window from LDS with
+// the same weights and the same summation order as upsample2_bwd_kernel (zero-weight terms add
+// +0, so the result is bit-identical).
+constexpr int UPB_TW = 32, UPB_TH = 8, UPB_FR = 2 * UPB_TH + 4, UPB_FC = 2 * UPB_TW + 4;
+__global__ __launch_bounds__(256) void upsample2_bwd_tile_kernel(const float* __restrict__ dy, int h,
+                                                                 int w, float ry, float rx,
+                                                                 float* __restrict__ dx) {
+  __shared__ float t[UPB_FR][UPB_FC + 1];
+  const int W2 = 2 * w, H2 = 2 * h;
+  const int ix0 = blockIdx.x * UPB_TW, iy0 = blockIdx.y * UPB_TH;
+  const int oyb = 2 * iy0 - 2, oxb = 2 * ix0 - 2;
+  const float* g = dy + (long)blockIdx.z * H2 * W2;
+  for (int e = threadIdx.x; e < UPB_FR * UPB_FC; e += 256) {
+    const int r = e / UPB_FC, c = e - r * UPB_FC;
+    const int oy = oyb + r, ox = oxb + c;
+    t[r][c] = (oy >= 0 && oy < H2 && ox >= 0 && ox < W2) ? g[oy * W2 + ox] : 0.f;
+  }
+  __syncthreads();
+  const int tx = threadIdx.x % UPB_TW, ty = threadIdx.x / UPB_TW;
+  const int ix = ix0 + tx, iy = iy0 + ty;
+  if (ix >= w || iy >= h) return;
+  int oy0, ox0;
+  float wy[6], wx[6];
+  up_adj_weights(iy, ry, h, H2, oy0, wy);
+  up_adj_weights(ix, rx, w, W2, ox0, wx);
+  float s = 0.f;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    float acc = 0.f;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) acc += wx[b] * t[2 * ty + a][2 * tx + b];
+    s += wy[a] * acc;
+  }
+  dx[(long)blockIdx.z * h * w + iy * w + ix] = s;
+}
+
 static inline float up_ratio(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
 
 int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStream_t st) {
@@ -827,8 +865,16 @@ int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStrea
 int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStream_t st) {
   const long n = (long)N * C * h * w;
   MD2_TRY(check_u31(4 * n));
-  hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, h, w,
-                     up_ratio(h, 2 * h), up_ratio(w, 2 * w), fd(w), fd(h), dx, (uint32_t)n);
+  static const int tiled = [] {
+    const char* e = getenv("MD2_UP_TILED");
+    return e ? atoi(e) : 1;
+  }();
+  if (tiled && (long)N * C <= 65535)
+    hipLaunchKernelGGL(upsample2_bwd_tile_kernel, dim3(cdiv(w, UPB_TW), cdiv(h, UPB_TH), N * C),
+                       dim3(256), 0, st, dy, h, w, up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx);
+  else
+    hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, h, w,
+                       up_ratio(h, 2 * h), up_ratio(w, 2 * w), fd(w), fd(h), dx, (uint32_t)n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
