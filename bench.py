@@ -141,7 +141,10 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    step()                                   # step 1 (warm-up): its loss is pinned by a test
+    torch.cuda.synchronize()
+    loss_first = loss_buf.item()
+    for _ in range(max(args.warmup - 1, 0)):
         step()
     barrier()
     t0 = time.perf_counter()
@@ -183,6 +186,7 @@ def main():
                        "batch_per_gpu": B, "global_batch": B * world, "height": H, "width": W,
                        "parallelism": f"dp{world}"},
             "loss": loss_val,
+            "loss_first_step": loss_first,   # == tests/golden/bench_first_loss.json (fp64 oracle) at B=12 416x128
         }
         if prof:
             ms, flop, n = prof["conv3x3_encoder"]

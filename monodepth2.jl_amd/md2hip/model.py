@@ -147,7 +147,15 @@ class _Executor:
         self.nseg = lib().md2_model_num_segments(h)
         self.automask = params.automasking
         self.forwarded = False
-        check(lib().md2_model_repack(h, stream_of(model.device)), "md2_model_repack")
+        self.version = -1                   # Model.version its packed conv weights reflect
+        self.sync()
+
+    def sync(self):
+        """Re-pack this executor's conv weights if the flat parameters changed since its last
+        pack (ADAM through another executor, load_flat, direct writes via Model.touch())."""
+        if self.version != self.model.version:
+            check(lib().md2_model_repack(self.handle, stream_of(self.model.device)), "md2_model_repack")
+            self.version = self.model.version
 
     def __del__(self):
         try:
@@ -174,6 +182,7 @@ class _Executor:
     def forward_loss(self, x, auto_loss=None, loss=None, terms=None):
         import torch
         loss = loss if loss is not None else torch.empty(1, dtype=torch.float32, device=x.device)
+        self.sync()
         am = auto_loss.contiguous() if (self.automask and auto_loss is not None) else None
         check(lib().md2_model_forward_loss(self.handle, ptr(x), ptr(am), ptr(loss), ptr(terms),
                                            stream_of(x.device)), "md2_model_forward_loss")
@@ -247,6 +256,10 @@ class Model:
         self.flat = flux_init(self.table, self.numel, seed).to(self.device, torch.float32)
         self.grad = torch.zeros_like(self.flat)
         self._ex: Dict[tuple, _Executor] = {}
+        self._last: Optional[_Executor] = None
+        # bumped whenever the flat parameters change; every executor keeps its own packed copy of
+        # the conv weights and re-packs lazily when it is behind (Model.executor / _Executor.sync)
+        self.version = 0
 
     # -- parameters (Flux.params(model)) ----------------------------------------------------
     def parameters(self) -> Dict[str, object]:
@@ -254,8 +267,18 @@ class Model:
 
     def load_flat(self, flat):
         self.flat.copy_(flat.to(self.flat.device, self.flat.dtype))
-        for ex in self._ex.values():
-            check(lib().md2_model_repack(ex.handle, stream_of(self.device)), "md2_model_repack")
+        self.touch()
+
+    def touch(self):
+        """Declare that ``flat`` was modified in place (the executors re-pack before next use)."""
+        self.version += 1
+
+    def evict(self, batch=None):
+        """Free the cached executors (all, or those of one batch size)."""
+        for k in [k for k in self._ex if batch is None or k[0] == batch]:
+            ex = self._ex.pop(k)
+            if ex is self._last:
+                self._last = None
 
     def executor(self, x_shape, cache: TrainCache, params: Params) -> _Executor:
         N, L, Cc, H, W = x_shape
@@ -268,7 +291,24 @@ class Model:
         if key not in self._ex:
             self._ex[key] = _Executor(self, N, H, W, cache, params)
         self._last = self._ex[key]
+        self._last.sync()
         return self._last
+
+    def eval_executor(self, N, H, W) -> _Executor:
+        """An executor of batch >= N at (H, W) for eval_disparity (the loss configuration does not
+        matter for inference); a new one (default TrainCache/Params) only if none fits."""
+        fits = [ex for k, ex in self._ex.items() if k[1] == H and k[2] == W and k[0] >= N]
+        if fits:
+            ex = min(fits, key=lambda e: e.batch)
+            ex.sync()
+            return ex
+        K, iK = depth10k_intrinsics(W, H)
+        cache = TrainCache(K=K, invK=iK)
+        params = Params(target_size=(W, H), batch_size=N, automasking=False)
+        key = (N, H, W, tuple(np.asarray(cache.K).reshape(-1)), tuple(cache.scales), params.min_depth,
+               params.max_depth, params.disparity_smoothness, params.automasking)
+        ex = self._ex[key] = _Executor(self, N, H, W, cache, params)   # leaves _last (training) alone
+        return ex
 
     def __call__(self, x, source_ids=(1, 3), target_id=2, cache: Optional[TrainCache] = None,
                  params: Optional[Params] = None):
@@ -330,9 +370,15 @@ class ADAM:
             self.m = torch.zeros_like(model.flat)
             self.v = torch.zeros_like(model.flat)
         self.t += 1
-        check(lib().md2_model_adam(model._last.handle, ptr(self.m), ptr(self.v), self.eta, self.beta[0],
+        ex = model._last
+        if ex is None:
+            raise RuntimeError("ADAM.update needs a preceding train_loss/gradient")
+        # md2_model_adam updates flat (shared by every executor) and re-packs ex's weights only
+        check(lib().md2_model_adam(ex.handle, ptr(self.m), ptr(self.v), self.eta, self.beta[0],
                                    self.beta[1], self.eps, self.t, grad_scale, stream_of(model.device)),
               "md2_model_adam")
+        model.touch()
+        ex.version = model.version
 
 
 def train_step(model: Model, x, auto_loss, cache: TrainCache, params: Params, opt: ADAM):
@@ -345,13 +391,13 @@ def train_step(model: Model, x, auto_loss, cache: TrainCache, params: Params, op
 
 def eval_disparity(model: Model, x, cache: Optional[TrainCache] = None):
     """``eval_disparity(m, x)`` (src/model.jl:63) for x [N, C, H, W] (train-mode BatchNorm, as
-    the reference never calls testmode!).  Uses an executor of batch >= N."""
+    the reference never calls testmode!).  Runs on any cached executor of batch >= N at (H, W)
+    (``Model.eval_executor``; its weights are re-packed first if stale); ``cache`` is unused
+    (inference has no loss) and kept for signature compatibility."""
     N, Cc, H, W = x.shape
-    if cache is None:
-        K, iK = depth10k_intrinsics(W, H)
-        cache = TrainCache(K=K, invK=iK)
-    params = Params(target_size=(W, H), batch_size=N, automasking=False)
-    ex = model.executor((N, 3, Cc, H, W), cache, params)
+    if Cc != model.encoder.in_channels:
+        raise ValueError("x must be [N, in_channels, H, W]")
+    ex = model.eval_executor(N, H, W)
     dptr = (C.c_void_p * 5)()
     check(lib().md2_model_eval_disparity(ex.handle, ptr(x), N, dptr, stream_of(x.device)),
           "md2_model_eval_disparity")

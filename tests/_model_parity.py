@@ -25,7 +25,8 @@ def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7):
     tail = md2hip.loss_tail([d.contiguous() for d in disps], poses_g, xg, None, cache, params, visualize=True)
     torch.cuda.synchronize()
     g = {"loss": loss.item(), "tail_loss": tail["loss"].item(), "disps": [d.cpu() for d in disps],
-         "pose": pose.cpu(), "grad": model.grad.cpu(), "sel": tail["vis_sel"].cpu()}
+         "pose": pose.cpu(), "grad": model.grad.cpu(), "sel": tail["vis_sel"].cpu(),
+         "flat": model.flat.detach().double().cpu()}
     g["decisions"] = gpu_decisions(model, N, arch)
     spec = O.param_spec(arch, C, (2, 3, 4, 5))
     flat = model.flat.detach().double().cpu().clone().requires_grad_(True)

@@ -73,6 +73,35 @@ CASES = [
     ((4, 8, 130, 256), 1, 3, 1, 1, False, None, True),           # zero padding, strip fwd/wgrad
     ((1, 16, 4, 64), 1, 3, 1, 1, True, "sigmoid", True),
     ((2, 64, 32, 104), 1, 3, 1, 1, True, "sigmoid", True),
+    # every conv of the benchmarked step (BASELINE config 3: B=12 triplets, 416x128) at its bench
+    # shape -- the encoder on 36 frames, the pose decoder on 24 pairs, the depth decoder on the 12
+    # targets -- so each planner choice the bench runs (tile, split-K count, stride-2 phase launch,
+    # wgrad kernel) is pinned against fp64
+    ((36, 3, 128, 416), 64, 7, 2, 3, False, None, False),        # stem 7x7/2
+    ((36, 64, 32, 104), 64, 3, 1, 1, False, None, False),        # layer1 3x3
+    ((36, 64, 32, 104), 128, 3, 2, 1, False, None, False),       # layer2.0.conv1 (stride 2)
+    ((36, 64, 32, 104), 128, 1, 2, 0, False, None, False),       # layer2.0 downsample
+    ((36, 128, 16, 52), 128, 3, 1, 1, False, None, False),       # layer2 3x3
+    ((36, 128, 16, 52), 256, 3, 2, 1, False, None, False),       # layer3.0.conv1
+    ((36, 128, 16, 52), 256, 1, 2, 0, False, None, False),       # layer3.0 downsample
+    ((36, 256, 8, 26), 256, 3, 1, 1, False, None, False),        # layer3 3x3
+    ((36, 256, 8, 26), 512, 3, 2, 1, False, None, False),        # layer4.0.conv1 (split-K)
+    ((36, 256, 8, 26), 512, 1, 2, 0, False, None, False),        # layer4.0 downsample
+    ((36, 512, 4, 13), 512, 3, 1, 1, False, None, False),        # layer4 3x3 (split-K)
+    ((36, 512, 4, 13), 256, 1, 1, 0, False, "relu", True),       # pose squeezer
+    ((24, 512, 4, 13), 256, 3, 1, 1, False, "relu", True),       # pose conv1
+    ((24, 256, 4, 13), 256, 3, 1, 1, False, "relu", True),       # pose conv2
+    ((24, 256, 4, 13), 6, 1, 1, 0, False, None, True),           # pose conv3
+    ((12, 512, 4, 13), 256, 3, 1, 1, True, "elu", True),         # branch1.c1
+    ((12, 512, 8, 26), 256, 3, 1, 1, True, "elu", True),         # branch1.c2 (256 up + 256 skip)
+    ((12, 256, 8, 26), 128, 3, 1, 1, True, "elu", True),         # branch2.c1
+    ((12, 256, 16, 52), 128, 3, 1, 1, True, "elu", True),        # branch2.c2
+    ((12, 128, 16, 52), 1, 3, 1, 1, True, "sigmoid", True),      # head2
+    ((12, 128, 16, 52), 64, 3, 1, 1, True, "elu", True),         # branch3.c1
+    ((12, 128, 32, 104), 64, 3, 1, 1, True, "elu", True),        # branch3.c2
+    ((12, 64, 32, 104), 1, 3, 1, 1, True, "sigmoid", True),      # head3
+    ((12, 64, 32, 104), 32, 3, 1, 1, True, "elu", True),         # branch4.c1
+    ((12, 32, 64, 208), 1, 3, 1, 1, True, "sigmoid", True),      # head4
 ]
 
 

@@ -188,3 +188,36 @@ def test_train_loss_visualization():
     md2hip.gradient(model)
     torch.cuda.synchronize()
     assert torch.isfinite(model.grad).all()
+
+
+def test_executors_see_updated_weights():
+    """Every cached executor keeps its own packed conv weights; after an ADAM step through one of
+    them the others must re-pack before use.  Sequence: train_loss + gradient at
+    N=2, eval_disparity at N=1 (a second executor, built between gradient() and update!),
+    ADAM update, then eval_disparity at N=1 and a forward at N=2 -- all against the oracle on the
+    UPDATED flat parameters."""
+    import md2hip
+    enc = md2hip.ResNet(18, in_channels=3)
+    m = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
+                                              embedding_levels=0), md2hip.PoseDecoder(512), seed=42)
+    K, invK = D.intrinsics(128, 64)
+    cache = md2hip.TrainCache(K=K.numpy(), invK=invK.numpy())
+    params = md2hip.Params(target_size=(128, 64), batch_size=2, automasking=False)
+    x2 = D.triplets(2, 3, 64, 128, seed=3).float().cuda()
+    x1 = D.triplets(1, 3, 64, 128, seed=4)[:, 1].contiguous()
+    opt = md2hip.ADAM(1e-3)                       # 10x Flux's step: stale weights are obvious
+    md2hip.train_loss(m, x2, None, cache, params)
+    md2hip.gradient(m)
+    before = md2hip.eval_disparity(m, x1.float().cuda())
+    opt.update(m)
+    after = md2hip.eval_disparity(m, x1.float().cuda())
+    P = O.unflatten(m.flat.double().cpu(), O.param_spec(18, 3, (2, 3, 4, 5)))
+    ref = O.eval_disparity(P, x1.float().double())
+    for s, (a, b) in enumerate(zip(after, ref)):
+        assert D.rel_err(a.cpu(), b) < 1e-5, s
+    assert D.rel_err(before[-1].cpu(), ref[-1]) > 1e-3       # the update did change the output
+    print(f"\nstale-vs-updated disparity difference {D.rel_err(before[-1].cpu(), ref[-1]):.3e}")
+    disps, _ = m(x2)
+    ref2, _ = O.model_forward(P, x2.cpu().double())
+    for s, (a, b) in enumerate(zip(disps, ref2)):
+        assert D.rel_err(a.cpu(), b) < 1e-5, s
