@@ -97,6 +97,79 @@ int md2_so3_compose_bwd(const float* pose, int n, int invert_mask, const float* 
                         float* d_pose, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Op-level loss primitives at ChainRulesCore rrule granularity (fwd + pullback pairs), for a host
+ * that differentiates the reference's ops one at a time (julia/MD2HIP.jl).  Layouts are the Julia
+ * arrays read as C-order; small matrices row-major (the shim passes permutedims).
+ *
+ * md2_automasking_loss   automasking_loss(ssim, x, target; source_ids)   src/training.jl:9-11
+ *   x [n][3][c][h][w]; out [n][h][w] = min over the two raw sources of photometric_loss (ties to
+ *   the first source); 0-based frame ids.  Not differentiable (data only).
+ * md2_ssim_{fwd,bwd}     (ssim::SSIM)(x, y)                                src/utils.jl:29-43
+ *   x, y, out, dout, dx, dy: [n][c][h][w] (Julia (W,H,C,N)); dx or dy may be NULL.
+ * md2_backproject_{fwd,bwd}   (b::Backproject)(depth, invK)                src/utils.jl:67-69
+ *   depth [n][w*h] (Julia (1,W*H,N)); out [n][w*h][3] (Julia (3,W*H,N)); invK row-major; the
+ *   invK cotangent is not formed (TrainCache constant).
+ * md2_project_{fwd,bwd}   (p::Project)(points, K, R, t)                    src/utils.jl:99-103
+ *   points [n][w*h][3]; R [n][9] row-major; t [n][3]; out [n][w*h][2] normalised (-1, 1);
+ *   pullback to points, R, t (deterministic per-sample reductions; K's cotangent not formed).
+ * md2_grid_sample_border_{fwd,bwd}   NNlib grid_sample(x, grid; padding_mode=:border),
+ *   align_corners=true (src/training.jl:56): x [n][c][hi][wi], grid [n][ho][wo][2] (Julia
+ *   (2,W,H,N)), out [n][c][ho][wo]; pullback to grid and (if d_x != NULL, by atomic scatter
+ *   whose summation order is not fixed) to x.
+ * md2_smooth_loss_{fwd,bwd}   smooth_loss(disparity, image)                 src/utils.jl:163-177
+ *   disparity [n][h][w], image [n][c][h][w] (c = 1 or 3); loss: one device float.
+ * md2_warp_photometric_{fwd,bwd}   one scale of train_loss's loop body     src/training.jl:43-62
+ *   upsample (align_corners) -> disparity_to_depth -> Backproject -> Project(R_s, t_s) ->
+ *   grid_sample(:border) -> photometric_loss per source -> min over sources [-> _apply_mask].
+ *   disp [n][dh][dw]; Rt [2][n][12] = composeT outputs (R row-major, t) of source 0 then 1
+ *   (md2_so3_compose_fwd); loss_map [n][h][w]; sel_map (NULL ok) = argmin (0/1, -1 automask).
+ *   Pullback of sum(d_loss .* loss_map): d_disp [n][dh][dw], d_Rt [2n][12] (each NULL ok).
+ * ---------------------------------------------------------------------------------------- */
+int md2_automasking_loss(const float* x, int n, int c, int h, int w, int target, int src0,
+                         int src1, float* out, void* stream);
+int md2_ssim_fwd(const float* x, const float* y, int n, int c, int h, int w, float* out,
+                 void* stream);
+int md2_ssim_bwd(const float* x, const float* y, const float* dout, int n, int c, int h, int w,
+                 float* dx, float* dy, void* stream);
+int md2_backproject_fwd(const float* depth, int n, int w, int h, const float* invK, float* out,
+                        void* stream);
+int md2_backproject_bwd(const float* dout, int n, int w, int h, const float* invK, float* d_depth,
+                        void* stream);
+int md2_project_fwd(const float* points, int n, int w, int h, const float* K, const float* R,
+                    const float* t, float* out, void* stream);
+size_t md2_project_workspace_size(int n, int w, int h);
+int md2_project_bwd(const float* points, int n, int w, int h, const float* K, const float* R,
+                    const float* t, const float* dout, float* d_points, float* d_R, float* d_t,
+                    void* workspace, void* stream);
+int md2_grid_sample_border_fwd(const float* x, const float* grid, int n, int c, int hi, int wi,
+                               int ho, int wo, float* out, void* stream);
+int md2_grid_sample_border_bwd(const float* x, const float* grid, const float* dout, int n, int c,
+                               int hi, int wi, int ho, int wo, float* d_grid, float* d_x,
+                               void* stream);
+size_t md2_smooth_loss_workspace_size(int n, int w, int h);
+int md2_smooth_loss_fwd(const float* disp, const float* img, int n, int c, int h, int w,
+                        float* loss, void* workspace, void* stream);
+int md2_smooth_loss_bwd(const float* disp, const float* img, int n, int c, int h, int w,
+                        float dloss, float* d_disp, void* workspace, void* stream);
+
+typedef struct md2_warp_cfg {
+  int n, c, width, height;       /* samples, channels, full (target) resolution              */
+  int dw, dh;                    /* resolution of the disparity of this scale                */
+  float K[9], invK[9];           /* row-major                                                 */
+  float min_depth, max_depth;    /* Params                                                    */
+  long long x_sample_stride;     /* elements between samples of x                            */
+  long long x_frame_stride;      /* elements between frames                                  */
+  int target, src0, src1;        /* 0-based frame ids                                        */
+} md2_warp_cfg;
+size_t md2_warp_photometric_workspace_size(const md2_warp_cfg* cfg);
+int md2_warp_photometric_fwd(const md2_warp_cfg* cfg, const float* disp, const float* Rt,
+                             const float* x, const float* automask, float* loss_map,
+                             signed char* sel_map, void* workspace, void* stream);
+int md2_warp_photometric_bwd(const md2_warp_cfg* cfg, const float* disp, const float* Rt,
+                             const float* x, const float* automask, const float* d_loss,
+                             float* d_disp, float* d_Rt, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * 2-D convolution (Flux Conv / NNlib conv, ∇conv_data, ∇conv_filter) on gfx950 fp32 MFMA.
  * x [n][cin][h][w], w [cout][cin][kh][kw] (cross-correlation; flip Flux kernels), bias [cout],
  * y [n][cout][ho][wo].  reflect=1: NNlib pad_reflect(x, pad) then a valid conv
@@ -180,7 +253,8 @@ size_t md2_model_device_bytes(md2_model* m);
 /* re-pack conv weights after the caller changed `params` directly */
 int md2_model_repack(md2_model* m, void* stream);
 /* forward (encoder on 3*batch frames, decoder on targets, poses) + train_loss value + the
- * loss-tail pullback; terms: [n_levels][2] or NULL */
+ * loss-tail pullback; terms: [n_levels][2] or NULL.  With cfg.automasking, auto_loss [batch][h][w]
+ * is the caller's automasking_loss, or NULL: the library computes it from x (md2_automasking_loss). */
 int md2_model_forward_loss(md2_model* m, const float* x, const float* auto_loss, float* loss,
                            float* terms, void* stream);
 /* backward in segments (0 = pose+depth decoders, 1..4 = layer4..layer1, 5 = stem); after

@@ -87,6 +87,46 @@ int md2_loss_fwd_bwd(const md2_loss_cfg* cfg, const float* const* disp, const fl
                        (hipStream_t)stream);
 }
 
+static WarpOpCfg to_warp_cfg(const md2_warp_cfg* c) {
+  WarpOpCfg w{};
+  w.N = c->n;
+  w.C = c->c;
+  w.W = c->width;
+  w.H = c->height;
+  w.dw = c->dw;
+  w.dh = c->dh;
+  std::memcpy(w.K, c->K, sizeof(w.K));
+  std::memcpy(w.invK, c->invK, sizeof(w.invK));
+  w.min_depth = c->min_depth;
+  w.max_depth = c->max_depth;
+  w.x_sample_stride = (long)c->x_sample_stride;
+  w.x_frame_stride = (long)c->x_frame_stride;
+  w.target = c->target;
+  w.src0 = c->src0;
+  w.src1 = c->src1;
+  return w;
+}
+
+size_t md2_warp_photometric_workspace_size(const md2_warp_cfg* cfg) {
+  return cfg ? warp_op_workspace_bytes(cfg->n, cfg->width, cfg->height) : 0;
+}
+
+int md2_warp_photometric_fwd(const md2_warp_cfg* cfg, const float* disp, const float* Rt,
+                             const float* x, const float* automask, float* loss_map,
+                             signed char* sel_map, void* workspace, void* stream) {
+  MD2_CHECK_ARG(cfg && loss_map, "warp_photometric_fwd: cfg/loss_map");
+  return warp_op_run(to_warp_cfg(cfg), disp, Rt, x, automask, nullptr, loss_map, sel_map, nullptr,
+                     nullptr, workspace, (hipStream_t)stream);
+}
+
+int md2_warp_photometric_bwd(const md2_warp_cfg* cfg, const float* disp, const float* Rt,
+                             const float* x, const float* automask, const float* d_loss,
+                             float* d_disp, float* d_Rt, void* workspace, void* stream) {
+  MD2_CHECK_ARG(cfg && d_loss, "warp_photometric_bwd: cfg/d_loss");
+  return warp_op_run(to_warp_cfg(cfg), disp, Rt, x, automask, d_loss, nullptr, nullptr, d_disp,
+                     d_Rt, workspace, (hipStream_t)stream);
+}
+
 int md2_so3_compose_fwd(const float* pose, int n, int invert_mask, float* Rt, void* stream) {
   MD2_CHECK_ARG(pose && Rt && n > 0, "so3 fwd args");
   return launch_so3_fwd(pose, 2 * n, n, invert_mask, Rt, (hipStream_t)stream);

@@ -27,6 +27,7 @@ struct PhotoArgs {
   const float* Rt;        // [2][N][12]  composed (R row-major, t) per (source, sample)
   const float* automask;  // [N][H][W] identity-reprojection loss or nullptr
   float wloss;            // d(total loss) / d(per-pixel warp loss)
+  const float* gmap;      // [N][H][W] per-pixel cotangent (times wloss) or nullptr (uniform)
   float* g_disp;          // [N][H][W] out: d loss / d full-res disparity (store)
   float* partials;        // [blocks][25]: loss sum, dR0(9) dt0(3), dR1(9) dt1(3)
   float* loss_map;        // [N][H][W] per-pixel warp loss (train_loss vis_loss) or nullptr
@@ -78,6 +79,10 @@ struct FinalizeArgs {
 };
 
 int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st);
+// identity-reprojection loss (training.jl:9-11): out [N][H][W] = min over the two raw sources of
+// photometric_loss(source, target)
+int launch_automask(const float* x, long x_sample_stride, long x_frame_stride, int target,
+                    int src0, int src1, int N, int C, int H, int W, float* out, hipStream_t st);
 // warped sources only (train_loss vis_warped): out [2][N][C][H][W]
 int launch_warp_vis(const PhotoArgs& a, const Geom& g, int C, float* out, hipStream_t st);
 long photometric_blocks(int W, int H, int N);
@@ -87,6 +92,8 @@ int launch_disp_sum(const float* disp, int dw, int dh, float rx, float ry, int W
 int launch_smooth(const SmoothArgs& a, int C, hipStream_t st);
 int launch_up_adjoint(const UpAdjArgs& a, hipStream_t st);
 int launch_loss_finalize(const FinalizeArgs& a, float* dRt, float* loss, hipStream_t st);
+// per-(source, sample) sums of the photometric blocks' pose partials -> dRt [2N][12]
+int launch_pose_grad_reduce(const FinalizeArgs& a, float* dRt, hipStream_t st);
 int launch_so3_fwd(const float* pose, int count, int N, int invert_mask, float* Rt,
                    hipStream_t st);
 int launch_so3_bwd(const float* pose, int count, int N, int invert_mask, const float* dRt,

@@ -324,6 +324,8 @@ __global__ __launch_bounds__(256) MD2_PHOTO_ATTR void photometric_kernel(PhotoAr
         wi[(dy + 1) * 3 + dx + 1] = ay * AW + ax;
       }
     const int ci = (by + 1) * AW + (bx + 1);     // centre in region A
+    // per-pixel cotangent of this window centre's loss (op-level pullback; 1 in train_loss)
+    const float gp = a.gmap ? a.gmap[((long)n * H + gy) * W + gx] : 1.f;
     float loss_s[2] = {0.f, 0.f};
     float coef1[NCOEF * C];                   // source 1 (source 0 goes straight to LDS)
 #pragma unroll
@@ -362,9 +364,10 @@ __global__ __launch_bounds__(256) MD2_PHOTO_ATTR void photometric_kernel(PhotoAr
         loss_s[s] += 0.85f / (float)C * sv + 0.15f / (float)C * fabsf(yc - xc);
         const float lv = (val >= 0.f && val <= 1.f) ? 1.f : 0.f;
         const float dn = -0.5f / den_ * lv, dd = 0.5f * num / (den_ * den_) * lv;
-        const float cq[NCOEF] = {kS * (dn * 2.f * my * A2 + dd * 2.f * mx * B2),  // d/d mu_x
-                                 kS * dd * B1,                                    // d/d var_x
-                                 kS * dn * 2.f * A1,                              // d/d cov_xy
+        const float kp = kS * gp;
+        const float cq[NCOEF] = {kp * (dn * 2.f * my * A2 + dd * 2.f * mx * B2),  // d/d mu_x
+                                 kp * dd * B1,                                    // d/d var_x
+                                 kp * dn * 2.f * A1,                              // d/d cov_xy
                                  mx, my};
 #pragma unroll
         for (int q = 0; q < NCOEF; ++q) {
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(256) MD2_PHOTO_ATTR void photometric_kernel(PhotoAr
       }
     }
     const int selq = s_sel[(ty + 1) * BW + (tx + 1)];
-    const float kL = a.wloss * 0.15f / (float)C;
+    const float kL = a.wloss * 0.15f / (float)C * (a.gmap ? a.gmap[((long)n * H + gy) * W + gx] : 1.f);
     float ddepth = 0.f;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -984,6 +987,12 @@ int launch_loss_finalize(const FinalizeArgs& a, float* dRt, float* loss, hipStre
     hipLaunchKernelGGL(pose_grad_reduce_kernel, dim3(2 * a.N), dim3(256), 0, st, a, dRt);
     MD2_LAUNCH_CHECK();
   }
+  return MD2_OK;
+}
+
+int launch_pose_grad_reduce(const FinalizeArgs& a, float* dRt, hipStream_t st) {
+  hipLaunchKernelGGL(pose_grad_reduce_kernel, dim3(2 * a.N), dim3(256), 0, st, a, dRt);
+  MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
 

@@ -163,4 +163,83 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
   return MD2_OK;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Op-level warp + photometric loss of ONE scale (src/training.jl:43-62): upsample the disparity,
+// depth, backproject, project with each composed pose, border grid_sample, SSIM + L1, min over
+// the two sources (and the automask).  Forward: the per-pixel warp_loss map; pullback: from a
+// per-pixel cotangent map to the disparity and to the composed poses Rt.
+// ---------------------------------------------------------------------------------------------
+size_t warp_op_workspace_bytes(int N, int W, int H) {
+  return align256(sizeof(float) * (size_t)N * W * H) +
+         align256(sizeof(float) * 25 * photometric_blocks(W, H, N));
+}
+
+int warp_op_run(const WarpOpCfg& c, const float* disp, const float* Rt, const float* x,
+                const float* automask, const float* d_loss, float* loss_map, signed char* sel_map,
+                float* d_disp, float* d_Rt, void* workspace, hipStream_t st) {
+  MD2_CHECK_ARG(c.N > 0 && c.W > 2 && c.H > 2 && c.dw >= 1 && c.dh >= 1 && c.dw <= c.W && c.dh <= c.H,
+                "warp_photometric dims");
+  MD2_CHECK_ARG(c.C == 1 || c.C == 3, "channels must be 1 or 3");
+  MD2_CHECK_ARG(disp && Rt && x && workspace, "warp_photometric: null pointer");
+  char* ws = (char*)workspace;
+  float* g_full = (float*)ws;
+  float* part = (float*)(ws + align256(sizeof(float) * (size_t)c.N * c.W * c.H));
+  Geom g;
+  std::memcpy(g.K, c.K, sizeof(g.K));
+  std::memcpy(g.invK, c.invK, sizeof(g.invK));
+  g.min_disp = (float)(1.0 / c.max_depth);
+  g.disp_range = (float)(1.0 / c.min_depth - 1.0 / c.max_depth);
+  g.W = c.W;
+  g.H = c.H;
+  g.wm1 = (float)(c.W - 1);
+  g.hm1 = (float)(c.H - 1);
+  PhotoArgs pa{};
+  pa.disp = disp;
+  pa.dw = c.dw;
+  pa.dh = c.dh;
+  pa.rx = ratio(c.dw, c.W);
+  pa.ry = ratio(c.dh, c.H);
+  pa.x = x;
+  pa.x_sample_stride = c.x_sample_stride;
+  pa.x_frame_stride = c.x_frame_stride;
+  pa.target = c.target;
+  pa.src0 = c.src0;
+  pa.src1 = c.src1;
+  pa.Rt = Rt;
+  pa.automask = automask;
+  pa.wloss = d_loss ? 1.f : 0.f;
+  pa.gmap = d_loss;
+  pa.g_disp = g_full;
+  pa.partials = part;
+  pa.loss_map = loss_map;
+  pa.sel_map = sel_map;
+  pa.N = c.N;
+  MD2_TRY(launch_photometric(pa, g, c.C, st));
+  if (!d_loss) return MD2_OK;
+  if (d_disp) {
+    UpAdjArgs ua{};
+    ua.g_full = g_full;
+    ua.disp = disp;
+    ua.dw = c.dw;
+    ua.dh = c.dh;
+    ua.rx = pa.rx;
+    ua.ry = pa.ry;
+    ua.out = d_disp;
+    ua.N = c.N;
+    ua.W = c.W;
+    ua.H = c.H;
+    MD2_TRY(launch_up_adjoint(ua, st));
+  }
+  if (d_Rt) {
+    FinalizeArgs fa{};
+    fa.nscales = 1;
+    fa.N = c.N;
+    fa.photo_partials[0] = part;
+    fa.photo_blocks[0] = photometric_blocks(c.W, c.H, c.N);
+    MD2_TRY(launch_pose_grad_reduce(fa, d_Rt, st));
+  }
+  return MD2_OK;
+}
+
 }  // namespace md2

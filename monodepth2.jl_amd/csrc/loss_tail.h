@@ -41,4 +41,19 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
                   const float* x, const float* automask, float dloss, const LossTailOut& o,
                   void* workspace, hipStream_t st);
 
+// Op-level per-scale warp + photometric loss (md2_warp_photometric_*).
+struct WarpOpCfg {
+  int N, C, W, H, dw, dh;
+  float K[9], invK[9];
+  float min_depth, max_depth;
+  long x_sample_stride, x_frame_stride;
+  int target, src0, src1;
+};
+size_t warp_op_workspace_bytes(int N, int W, int H);
+// d_loss == nullptr: forward only (loss_map / sel_map); else also the pullback of sum(d_loss .*
+// warp_loss) into d_disp [N][dh][dw] and d_Rt [2N][12] (each optional).
+int warp_op_run(const WarpOpCfg& c, const float* disp, const float* Rt, const float* x,
+                const float* automask, const float* d_loss, float* loss_map, signed char* sel_map,
+                float* d_disp, float* d_Rt, void* workspace, hipStream_t st);
+
 }  // namespace md2

@@ -254,6 +254,7 @@ class Model {
   void* tail_ws = nullptr;
   LossTailCfg tail{};
   float* loss_buf = nullptr;
+  float* amask = nullptr;       // automasking_loss of the current batch when the caller passes none
   const float* eval_disp[MAX_SCALES] = {};
 
   ~Model() {
@@ -506,6 +507,7 @@ class Model {
       tail_ws = q;
     }
     MD2_TRY(alloc(&loss_buf, 16));
+    if (cfg.automask) MD2_TRY(alloc(&amask, (long)N * cfg.H * cfg.W));
     return build_pack_table();
   }
 
@@ -735,6 +737,13 @@ class Model {
     if (prof) {
       for (int k = 0; k < 2 * tail.nscales; ++k) pev[k] = ev();
       o.photo_events = pev;
+    }
+    if (cfg.automask && !automask) {
+      // automasking_loss(ssim, x, target; source_ids) (src/training.jl:9-11): identity
+      // reprojection of the raw sources, the third candidate of every scale's per-pixel min
+      MD2_TRY(launch_automask(x, tail.x_sample_stride, tail.x_frame_stride, tail.target, tail.src0,
+                              tail.src1, N, cfg.arch.in_ch, cfg.H, cfg.W, amask, st));
+      automask = amask;
     }
     MD2_TRY(loss_tail_run(tail, disps, pose, x, cfg.automask ? automask : nullptr, 1.f, o, tail_ws, st));
     if (prof) {
@@ -974,7 +983,6 @@ void model_destroy(Model* m) { delete m; }
 int model_forward_loss(Model* m, const float* x, const float* automask, float* loss, float* terms,
                        hipStream_t st) {
   MD2_CHECK_ARG(m && x, "model/x");
-  MD2_CHECK_ARG(!m->cfg.automask || automask, "automasking needs auto_loss");
   m->cur_x = x;
   return m->forward_loss(x, automask, loss, terms, st);
 }

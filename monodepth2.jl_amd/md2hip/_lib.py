@@ -57,6 +57,18 @@ class ModelCfg(C.Structure):
     ]
 
 
+class WarpCfg(C.Structure):
+    """``md2_warp_cfg``."""
+    _fields_ = [
+        ("n", C.c_int), ("c", C.c_int), ("width", C.c_int), ("height", C.c_int),
+        ("dw", C.c_int), ("dh", C.c_int),
+        ("K", C.c_float * 9), ("invK", C.c_float * 9),
+        ("min_depth", C.c_float), ("max_depth", C.c_float),
+        ("x_sample_stride", C.c_longlong), ("x_frame_stride", C.c_longlong),
+        ("target", C.c_int), ("src0", C.c_int), ("src1", C.c_int),
+    ]
+
+
 _lib = None
 _load_error = None
 
@@ -105,6 +117,23 @@ _SIGS = {
     "md2_mpi_embed_features": (C.c_int, [P, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int,
                                          C.c_int, P, P]),
     "md2_concat_channels": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_longlong, P, P]),
+    "md2_automasking_loss": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "md2_ssim_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "md2_ssim_bwd": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
+    "md2_backproject_fwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, P, P, P]),
+    "md2_backproject_bwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, P, P, P]),
+    "md2_project_fwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, P, P, P, P, P]),
+    "md2_project_workspace_size": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    "md2_project_bwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P, P, P]),
+    "md2_grid_sample_border_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "md2_grid_sample_border_bwd": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                             P, P, P]),
+    "md2_smooth_loss_workspace_size": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    "md2_smooth_loss_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
+    "md2_smooth_loss_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, P, P, P]),
+    "md2_warp_photometric_workspace_size": (C.c_size_t, [C.POINTER(WarpCfg)]),
+    "md2_warp_photometric_fwd": (C.c_int, [C.POINTER(WarpCfg), P, P, P, P, P, P, P, P]),
+    "md2_warp_photometric_bwd": (C.c_int, [C.POINTER(WarpCfg), P, P, P, P, P, P, P, P, P]),
     "md2_model_set_profiling": (C.c_int, [P, C.c_int]),
     "md2_model_profile_read": (C.c_int, [P, C.POINTER(C.c_double), C.c_int]),
 }

@@ -115,8 +115,9 @@ def loss_tail(disparities, poses, x, auto_loss, cache: TrainCache, params: Param
         res["vis_warped"] = torch.empty(2, N, C_, H, W, dtype=torch.float32, device=dev)
     am = None
     if params.automasking:
-        if auto_loss is None:
-            raise ValueError("Params.automasking=true needs auto_loss")
+        if auto_loss is None:        # automasking_loss(ssim, x, target; source_ids), on the GPU
+            from .primitives import automasking_loss
+            auto_loss = automasking_loss(x, cache.target_id, cache.source_ids)
         am = auto_loss.contiguous()
     out = _lib.LossOut()
     out.loss = res["loss"].data_ptr()

@@ -7,7 +7,7 @@ from oracle import md2_oracle as O
 from tests import _data as D
 
 
-def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7):
+def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, automasking=False):
     x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
     K, invK = D.intrinsics(W, H)
     enc = md2hip.ResNet(arch, in_channels=C)
@@ -15,7 +15,7 @@ def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7):
                                                   embedding_levels=0),
                          md2hip.PoseDecoder(enc.stages[-1]), seed=42)
     cache = md2hip.TrainCache(K=K.numpy(), invK=invK.numpy())
-    params = md2hip.Params(target_size=(W, H), batch_size=N, automasking=False)
+    params = md2hip.Params(target_size=(W, H), batch_size=N, automasking=automasking)
     xg = x.float().cuda().contiguous()
     loss, *_ = md2hip.train_loss(model, xg, None, cache, params)
     disps, pose = model._last.outputs()
@@ -34,9 +34,11 @@ def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7):
     with O.forced_decisions(g["decisions"]):
         d_o, p_o = O.model_forward(P, x, arch=arch)
     cache_o = O.TrainCache(K=K, invK=invK)
-    par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
-    forced = [g["sel"][s].unsqueeze(1).long() for s in range(4)]
-    loss_o = O.loss_from_outputs(d_o, p_o, x, None, cache_o, par_o, forced_sel=forced)
+    par_o = O.Params(target_size=(W, H), batch_size=N, automasking=automasking)
+    # the GPU's argmin (-1 = automask) as an index into [auto_loss?, source 0, source 1]
+    forced = [g["sel"][s].unsqueeze(1).long() + (1 if automasking else 0) for s in range(4)]
+    auto_o = O.automasking_loss(x, x[:, 1], (1, 3)) if automasking else None
+    loss_o = O.loss_from_outputs(d_o, p_o, x, auto_o, cache_o, par_o, forced_sel=forced)
     loss_o.backward()
     o = {"loss": loss_o.item(), "disps": [d.detach() for d in d_o],
          "pose": torch.cat([torch.cat([r, t], 1) for r, t in p_o], 0).detach(), "grad": flat.grad}
