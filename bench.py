@@ -43,6 +43,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-probe", action="store_true", help="skip the HIP-event roofline probe")
+    ap.add_argument("--comm", choices=("md2", "torch"), default="md2",
+                    help="gradient all-reduce for N > 1: the library's own RCCL communicator "
+                         "(md2_comm_*, gloo only as the host control plane) or torch.distributed nccl")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="run the data-parallel step (process group, all-reduce) even at N = 1")
     return ap.parse_args()
 
 
@@ -103,21 +108,34 @@ def pmc_traffic():
 
 def main():
     args = parse()
+    # libraries print banners on fd 1 (RCCL's version block, gloo's peer count): keep stdout for
+    # the ONE JSON line -- everything else goes to stderr until it is printed
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    dp = world > 1 or args.force_dp
+    if dp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.comm == "md2":
+            dist.init_process_group("gloo")            # host control plane only
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
     import md2hip
+    import md2hip.comm
     import md2hip.dist
     B, H, W = args.batch, args.height, args.width
     enc = md2hip.ResNet(args.arch, in_channels=3)
@@ -131,13 +149,20 @@ def main():
     x = synthetic_batch(B, H, W, rank, dev)
     ex = model.executor(tuple(x.shape), cache, params)
     loss_buf = torch.empty(1, dtype=torch.float32, device=dev)
-    comm = md2hip.dist.GradAllReduce()
+    if dp and args.comm == "md2":
+        comm = md2hip.comm.Comm(rank, world, md2hip.comm.broadcast_id(rank), local)
 
-    def step():
-        md2hip.dist.train_step(ex, model, opt, x, comm, loss=loss_buf)
+        def step():
+            md2hip.comm.train_step_dp(ex, model, opt, x, comm, loss=loss_buf)
+    else:
+        comm = md2hip.dist.GradAllReduce(force=args.force_dp)
+
+        def step():
+            md2hip.dist.train_step(ex, model, opt, x, comm, loss=loss_buf)
 
     def barrier():
-        if world > 1:
+        torch.cuda.synchronize()
+        if dp:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -152,8 +177,8 @@ def main():
         step()
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dp:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.comm == "torch" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     loss_val = loss_buf.item()
@@ -184,7 +209,9 @@ def main():
                     "Flux-default random init (seed 42)",
             "config": {"workload": f"train_step resnet{args.arch} depth+pose decoders, 4-scale photometric loss, ADAM",
                        "batch_per_gpu": B, "global_batch": B * world, "height": H, "width": W,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "allreduce": ("rccl md2_comm (bucketed, overlapped with backward)" if args.comm == "md2"
+                                     else "rccl torch.distributed (bucketed, overlapped)") if dp else None},
             "loss": loss_val,
             "loss_first_step": loss_first,   # == tests/golden/bench_first_loss.json (fp64 oracle) at B=12 416x128
         }
@@ -212,8 +239,11 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
             except Exception as e:  # pragma: no cover - report, never fake
                 out["cpu_baseline"] = {"error": repr(e)}
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    if dp:
+        if args.comm == "md2":
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -275,6 +275,30 @@ int md2_model_adam(md2_model* m, float* adam_m, float* adam_v, float lr, float b
 /* forward_loss + every backward segment + ADAM (single-GPU step) */
 int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, float* adam_m,
                          float* adam_v, float lr, int step, float* loss, void* stream);
+/* ------------------------------------------------------------------------------------------
+ * Data parallelism over RCCL (xGMI), one process (rank) per GPU -- SURVEY.md 8(e).  The
+ * reference has no collectives; these replace the torch.distributed plumbing so a Julia host
+ * needs only this library.  RCCL is dlopen'ed on first use (MD2_ENOTSUP if absent).
+ * md2_comm_get_unique_id: rank 0 creates the 128-byte id and ships it to the other ranks (file,
+ * MPI, a TCP store ...); md2_comm_init then joins (collective over all ranks) on `device`.
+ * md2_model_backward_allreduce: every backward segment on `stream`, each followed by the RCCL
+ * sum of its (final) gradient range on the communicator's own stream -- bucketed, overlapped with
+ * the rest of the backward; `stream` waits for all buckets before returning.  comm == NULL:
+ * plain backward.  md2_model_train_step_dp: forward_loss + that + ADAM with grad_scale 1/nranks.
+ * ---------------------------------------------------------------------------------------- */
+#define MD2_COMM_ID_BYTES 128
+typedef struct md2_comm md2_comm;
+int md2_comm_get_unique_id(char* id);
+int md2_comm_init(int rank, int nranks, const char* id, int device, md2_comm** out);
+int md2_comm_destroy(md2_comm* comm);
+int md2_comm_rank(const md2_comm* comm, int* rank, int* nranks);
+/* in-place sum all-reduce of n floats, on `stream` (RCCL's ordering) */
+int md2_comm_allreduce_sum(md2_comm* comm, float* buf, long long n, void* stream);
+int md2_model_backward_allreduce(md2_model* m, md2_comm* comm, void* stream);
+int md2_model_train_step_dp(md2_model* m, md2_comm* comm, const float* x, const float* auto_loss,
+                            float* adam_m, float* adam_v, float lr, float beta1, float beta2,
+                            float eps, int step, float* loss, void* stream);
+
 /* device pointers of the last forward: disparities per level and poses [2*batch][6] */
 int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose);
 /* The five encoder stage outputs of the last forward (device memory owned by the model):

@@ -298,10 +298,6 @@ int md2_arch_param_info(const md2_model_cfg* cfg, int idx, char* name, int name_
   return MD2_OK;
 }
 
-struct md2_model {
-  Model* impl;
-};
-
 int md2_model_create(const md2_model_cfg* c, float* params, float* grads, md2_model** out) {
   MD2_CHECK_ARG(c && params && grads && out, "model_create args");
   ModelCfg mc;

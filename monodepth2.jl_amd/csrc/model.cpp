@@ -1126,6 +1126,7 @@ int model_profile_read(Model* m, double* out, int ncat) {
 }
 
 long model_param_count(Model* m) { return m ? m->spec.total : 0; }
+float* model_grads(Model* m) { return m ? m->grads : nullptr; }
 size_t model_device_bytes(Model* m) { return m ? m->bytes : 0; }
 
 }  // namespace md2

@@ -67,6 +67,12 @@ int model_features(Model* m, const float** feat, int* c, int* h, int* w);
 int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipStream_t st);
 int model_debug_tensor(Model* m, int index, const char** name, const void** ptr, int* dims);
 long model_param_count(Model* m);
+float* model_grads(Model* m);          // the caller-owned flat gradient vector
 size_t model_device_bytes(Model* m);
 
 }  // namespace md2
+
+// opaque handle of the C ABI (include/md2.h)
+struct md2_model {
+  md2::Model* impl;
+};

@@ -38,18 +38,28 @@ def synthetic_triplets(batch: int, height: int, width: int, first_index: int, de
 class GradAllReduce:
     """Overlapped bucket all-reduce of slices of one flat gradient vector."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force: bool = False):
         import torch.distributed as dist
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if on else 1
+        self.backend = dist.get_backend(group) if on else None
+        self.force = force and on           # run the collective even at world size 1 (tests)
         self._handles: List = []
 
     def bucket_ready(self, flat_grad, off: int, length: int):
         """Launch the sum all-reduce of flat_grad[off:off+length] (returns immediately)."""
-        if self.world == 1 or length == 0:
+        if (self.world == 1 and not self.force) or length == 0:
             return
         import torch.distributed as dist
-        self._handles.append(dist.all_reduce(flat_grad[off:off + length], group=self.group, async_op=True))
+        sl = flat_grad[off:off + length]
+        if self.backend == "gloo" and sl.is_cuda:
+            # host control-plane backend (CPU tests, same-device rehearsal): stage through the host
+            h = sl.cpu()
+            dist.all_reduce(h, group=self.group)
+            sl.copy_(h)
+            return
+        self._handles.append(dist.all_reduce(sl, group=self.group, async_op=True))
 
     def wait(self):
         """Make the current stream wait for every launched bucket."""
