@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--width", type=int, default=416)
     ap.add_argument("--arch", type=int, default=18)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-probe", action="store_true", help="skip the HIP-event roofline probe")
     ap.add_argument("--comm", choices=("md2", "torch"), default="md2",
                     help="gradient all-reduce for N > 1: the library's own RCCL communicator "
@@ -57,13 +57,71 @@ def synthetic_batch(batch, height, width, rank, device):
     return synthetic_triplets(batch, height, width, rank * batch, device)
 
 
+def _host_cpu():
+    """Host CPU model, logical CPU count of the machine and the CPUs this process may run on."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    # a container's CPU quota (cgroup v2 cpu.max / v1 cfs quota) caps the usable cores below
+    # what the affinity mask shows: more threads than that only oversubscribe the quota
+    quota = None
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", lambda t: [t.strip(), None])):
+        try:
+            with open(path) as f:
+                q, p = parse(f.read())
+            if q not in ("max", "-1"):
+                if p is None:
+                    with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                        p = f.read().strip()
+                quota = max(1, int(int(q) // int(p)))
+            break
+        except (OSError, ValueError):
+            continue
+    if quota is not None:
+        avail = min(avail, quota)
+    return model, os.cpu_count() or 1, avail
+
+
+def _median_time(fn, warmup, min_steps, seconds):
+    """2 untimed warm-ups, then the median of >= min_steps timed calls (more while time allows)."""
+    import statistics
+    for _ in range(warmup):
+        fn()
+    times = []
+    t_end = time.perf_counter() + seconds
+    while len(times) < min_steps or time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+        print(f"cpu baseline: step {len(times)} {times[-1]:.2f} s", file=sys.stderr, flush=True)
+        if len(times) >= 50:
+            break
+    return statistics.median(times), len(times)
+
+
 def cpu_baseline(args, seconds):
     """The oracle (torch-CPU fp32 restatement of the reference step, oracle/md2_oracle.py) on the
-    host cores: forward + train_loss + autograd backward + Flux ADAM, same shapes/batch."""
+    host cores: forward + train_loss + autograd backward + Flux ADAM (BASELINE config 3), and
+    eval_disparity (config 2), same shapes and batch.  Threads = every CPU this process may run on
+    (the box's per-GPU CPU share; `nproc` reports the whole machine)."""
     import torch
     from oracle import md2_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    model, nproc, avail = _host_cpu()
+    threads = avail
     torch.set_num_threads(threads)
+    print(f"cpu baseline: {threads} threads ({nproc} logical CPUs on the host, {model})",
+          file=sys.stderr, flush=True)
     B, H, W = args.batch, args.height, args.width
     spec = O.param_spec(args.arch, 3, (2, 3, 4, 5))
     flat = O.init_params(spec, 42, dtype=torch.float32).requires_grad_(True)
@@ -81,14 +139,22 @@ def cpu_baseline(args, seconds):
             opt.step("flat", flat, g)
         return loss.item()
 
-    step()                                    # untimed warm-up
-    n, t0 = 0, time.perf_counter()
-    while n < 1 or (time.perf_counter() - t0 < seconds and n < 5):
-        step()
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n * B / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} full train step(s) at batch {B} {W}x{H} (fp32 torch-CPU oracle, after 1 warm-up)"}
+    t, n = _median_time(step, 2, 5, seconds)
+    out = {"value": round(B / t, 3), "unit": "images/s", "cores": threads, "kind": "port",
+           "nproc": nproc, "cpu_model": model,
+           "sample": f"median of {n} full train steps at batch {B} {W}x{H} after 2 warm-ups "
+                     f"(fp32 torch-CPU restatement of the Flux/Zygote reference, oracle/md2_oracle.py; "
+                     f"baseline only)"}
+
+    def evald():
+        with torch.no_grad():
+            P = O.unflatten(flat.detach(), spec)
+            O.eval_disparity(P, x[:, 1].contiguous(), arch=args.arch)
+
+    t2, n2 = _median_time(evald, 2, 5, seconds / 3)
+    out["eval_disparity"] = {"value": round(B / t2, 3), "unit": "images/s",
+                             "sample": f"median of {n2} eval_disparity calls at batch {B} (BASELINE config 2)"}
+    return out
 
 
 def pmc_traffic():
@@ -104,6 +170,22 @@ def pmc_traffic():
     if not t:
         return None, None
     return round(t["bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+
+
+def pmc_photo_traffic(batch):
+    """HBM bytes per launch of the photometric kernel at this batch from the newest committed
+    tools/pmc_photo.sh profile (profiles/r*_pmc_photo.json; FETCH doubled per the gfx950 note,
+    uncalibrated for 4-byte gathers) -- PMC cannot run inside the timed bench."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_photo.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    row = d.get("by_batch", {}).get(str(batch))
+    if not row or d.get("scales_per_launch") != 4:
+        return None, None
+    return row["traffic_bytes"], os.path.relpath(files[-1], ROOT)
 
 
 def main():
@@ -226,9 +308,12 @@ def main():
                                "launches": n, "algorithmic_flop_per_step": flop, "kernel_ms_per_step": round(ms, 4)}
             ms, byt, n = prof["photometric"]
             gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-            out["roofline_photometric"] = {"bound": "hbm", "kernel": "photometric_kernel (fused warp+SSIM+L1 fwd+bwd)",
+            ptraffic, psrc = pmc_photo_traffic(B)
+            out["roofline_photometric"] = {"bound": "hbm", "kernel": "photo_stream_kernel (fused warp+SSIM+L1 fwd+bwd, all 4 scales in one launch)",
                                            "achieved": round(gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                           "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                                           "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": ptraffic,
+                                           "traffic_source": psrc,
+                                           "note": "VALU-issue bound, not HBM-bound: profiles/r02_pmc_photo.json",
                                            "launches": n, "algorithmic_bytes_per_step": byt,
                                            "kernel_ms_per_step": round(ms, 4)}
             ms2, flop2, n2 = prof["conv_other"]

@@ -1,0 +1,436 @@
+# MD2HIP.jl -- the Julia host binding of libmd2hip.so (include/md2.h) for Monodepth2.jl.
+#
+# Drop-in for the reference's GPU hot path: `include("MD2HIP.jl")` from src/Monodepth.jl (after
+# `using AMDGPU, ChainRulesCore`), then use MD2HIP.HIPModel / MD2HIP.train_loss where the reference
+# uses Model / train_loss (src/training.jl:21-78, scripts/script.jl:84-86).  Every op below is a
+# forward `ccall` plus a `ChainRulesCore.rrule` whose pullback is the library's hand-written HIP
+# pullback -- the reference's own plugin mechanism (src/utils.jl:134-145, src/repeat.jl:44-69).
+#
+# Julia is not installed in the build container: this file is the binding a maintainer adds; the
+# Python mirror monodepth2.jl_amd/md2hip/ makes the same calls and is what the tests execute.
+#
+# Layout contract (INTEGRATION.md): Julia column-major (W,H,C,N) arrays have the bytes of the
+# library's C-order [n][c][h][w]; 3x3 matrices go row-major (`vec(permutedims(K))`); Flux Conv
+# weights (kw,kh,cin,cout) are true convolutions -> flipped once into the library's
+# cross-correlation layout by `flat_params`.
+module MD2HIP
+
+using AMDGPU
+using ChainRulesCore
+
+const lib = get(ENV, "MD2HIP_LIB",
+                joinpath(@__DIR__, "..", "monodepth2.jl_amd", "lib", "libmd2hip.so"))
+
+check(rc) = rc == 0 || error("libmd2hip (", rc, "): ",
+                             unsafe_string(ccall((:md2_last_error, lib), Cstring, ())))
+stream_ptr() = AMDGPU.stream().stream                  # hipStream_t of the task-local stream
+rowmajor(M) = ntuple(i -> Float32(M[(i - 1) ÷ 3 + 1, (i - 1) % 3 + 1]), 9)
+pad5(v, T) = ntuple(i -> i <= length(v) ? T(v[i]) : zero(T), 5)
+ptr(a) = a === nothing ? C_NULL : pointer(a)
+
+# ------------------------------------------------------------------------------------------------
+# C structs (field order and types exactly as include/md2.h)
+# ------------------------------------------------------------------------------------------------
+struct ModelCfg                                        # md2_model_cfg
+    arch::Cint; in_channels::Cint; batch::Cint; width::Cint; height::Cint
+    n_levels::Cint; scale_levels::NTuple{5,Cint}
+    K::NTuple{9,Cfloat}; invK::NTuple{9,Cfloat}
+    min_depth::Cfloat; max_depth::Cfloat; disparity_smoothness::Cfloat
+    scales::NTuple{5,Cfloat}; automasking::Cint
+    target::Cint; src0::Cint; src1::Cint
+end
+
+# Params / TrainCache of src/Monodepth.jl:37-60 -> md2_model_cfg
+function ModelCfg(arch, in_ch, scale_levels, p, c)
+    ModelCfg(arch, in_ch, p.batch_size, p.target_size..., length(scale_levels),
+             pad5(scale_levels, Cint), rowmajor(c.K), rowmajor(c.invK),
+             p.min_depth, p.max_depth, p.disparity_smoothness, pad5(c.scales, Cfloat),
+             p.automasking, c.target_id - 1, c.source_ids[1] - 1, c.source_ids[2] - 1)
+end
+
+struct LossCfg                                         # md2_loss_cfg
+    n::Cint; c::Cint; width::Cint; height::Cint; nscales::Cint
+    scale_w::NTuple{5,Cint}; scale_h::NTuple{5,Cint}
+    smooth_weight::NTuple{5,Cfloat}; divisor::Cfloat; smooth_normalize::Cint
+    K::NTuple{9,Cfloat}; invK::NTuple{9,Cfloat}
+    min_depth::Cfloat; max_depth::Cfloat
+    x_sample_stride::Clonglong; x_frame_stride::Clonglong
+    target::Cint; src0::Cint; src1::Cint; invert_mask::Cint; sigmoid_grad::Cint
+end
+
+struct LossOut                                         # md2_loss_out
+    loss::Ptr{Float32}; terms::Ptr{Float32}
+    d_disp::NTuple{5,Ptr{Float32}}; d_pose::Ptr{Float32}
+    vis_loss::Ptr{Float32}; vis_sel::Ptr{Int8}; vis_warped::Ptr{Float32}
+end
+
+struct WarpCfg                                         # md2_warp_cfg
+    n::Cint; c::Cint; width::Cint; height::Cint; dw::Cint; dh::Cint
+    K::NTuple{9,Cfloat}; invK::NTuple{9,Cfloat}
+    min_depth::Cfloat; max_depth::Cfloat
+    x_sample_stride::Clonglong; x_frame_stride::Clonglong
+    target::Cint; src0::Cint; src1::Cint
+end
+
+struct ConvDesc                                        # md2_conv_desc
+    n::Cint; cin::Cint; h::Cint; w::Cint; cout::Cint; kh::Cint; kw::Cint
+    stride::Cint; pad::Cint; reflect::Cint; act::Cint
+end
+
+# ------------------------------------------------------------------------------------------------
+# The model: Model(ResidualNetwork, DepthDecoder, PoseDecoder) with its parameters in ONE flat
+# device vector (Flux `params(model)` order, md2_arch_param_info) -- src/model.jl:24-70
+# ------------------------------------------------------------------------------------------------
+mutable struct HIPModel
+    handle::Ptr{Cvoid}
+    cfg::ModelCfg
+    θ::ROCVector{Float32}
+    ∇θ::ROCVector{Float32}
+    m::ROCVector{Float32}; v::ROCVector{Float32}; step::Int
+end
+
+function param_count(cfg::ModelCfg)
+    ne, nel = Ref{Clonglong}(), Ref{Clonglong}()
+    check(ccall((:md2_arch_param_count, lib), Cint, (Ref{ModelCfg}, Ref{Clonglong}, Ref{Clonglong}),
+                cfg, ne, nel))
+    return Int(ne[]), Int(nel[])
+end
+
+# (name, shape, 0-based offset) of table entry i (0-based)
+function param_info(cfg::ModelCfg, i)
+    name = Vector{UInt8}(undef, 128); nd = Ref{Cint}(); shape = zeros(Cint, 4); off = Ref{Clonglong}()
+    check(ccall((:md2_arch_param_info, lib), Cint,
+                (Ref{ModelCfg}, Cint, Ptr{UInt8}, Cint, Ref{Cint}, Ptr{Cint}, Ref{Clonglong}),
+                cfg, i, name, length(name), nd, shape, off))
+    return unsafe_string(pointer(name)), Tuple(Int.(shape[1:nd[]])), Int(off[])
+end
+
+# Flux params -> the library's flat vector: conv weights (kw,kh,cin,cout) flipped in both spatial
+# axes (true convolution -> cross-correlation); everything else copied as is.  `ps` iterates in
+# Flux `params(model)` order, which is the table order.
+function flat_params(cfg::ModelCfg, ps)
+    ne, nel = param_count(cfg)
+    flat = Vector{Float32}(undef, nel)
+    for (i, p) in enumerate(ps)
+        name, shape, off = param_info(cfg, i - 1)
+        length(p) == prod(shape) || error("parameter $name: Flux size $(size(p)) vs table $shape")
+        a = Array{Float32}(p)
+        ndims(a) == 4 && (a = a[end:-1:1, end:-1:1, :, :])
+        flat[off+1:off+length(a)] = vec(a)
+    end
+    ne == length(collect(ps)) || error("Flux model has a different parameter count than the table")
+    return ROCVector{Float32}(flat)
+end
+
+function HIPModel(cfg::ModelCfg, θ::ROCVector{Float32})
+    ∇θ = similar(θ); h = Ref{Ptr{Cvoid}}()
+    check(ccall((:md2_model_create, lib), Cint,
+                (Ref{ModelCfg}, Ptr{Float32}, Ptr{Float32}, Ref{Ptr{Cvoid}}), cfg, θ, ∇θ, h))
+    m = HIPModel(h[], cfg, θ, ∇θ, fill!(similar(θ), 0), fill!(similar(θ), 0), 0)
+    check(ccall((:md2_model_repack, lib), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), m.handle, stream_ptr()))
+    finalizer(x -> ccall((:md2_model_destroy, lib), Cint, (Ptr{Cvoid},), x.handle), m)
+end
+
+# (m)(x, source_ids, target_id) -- disparities (Julia (w,h,1,n) views of library memory) and
+# poses of the last forward (src/model.jl:24-55)
+function outputs(m::HIPModel)
+    d = Vector{Ptr{Float32}}(undef, 5); w = zeros(Cint, 5); h = zeros(Cint, 5); pose = Ref{Ptr{Float32}}()
+    check(ccall((:md2_model_outputs, lib), Cint,
+                (Ptr{Cvoid}, Ptr{Ptr{Float32}}, Ptr{Cint}, Ptr{Cint}, Ref{Ptr{Float32}}),
+                m.handle, d, w, h, pose))
+    n = m.cfg.batch
+    disps = [unsafe_wrap(ROCArray, d[k], (Int(w[k]), Int(h[k]), 1, n)) for k in 1:m.cfg.n_levels]
+    return disps, unsafe_wrap(ROCArray, pose[], (6, 2n))
+end
+
+# the loss-tail config of this model (for the visualisation pass)
+function loss_cfg(m::HIPModel)
+    c = m.cfg; disps, _ = outputs(m)
+    LossCfg(c.batch, c.in_channels, c.width, c.height, c.n_levels,
+            pad5([size(d, 1) for d in disps], Cint), pad5([size(d, 2) for d in disps], Cint),
+            pad5([c.disparity_smoothness * s for s in c.scales[1:c.n_levels]], Cfloat),
+            Float32(c.n_levels), 1, c.K, c.invK, c.min_depth, c.max_depth,
+            3 * c.in_channels * c.height * c.width, c.in_channels * c.height * c.width,
+            c.target, c.src0, c.src1, (c.src0 < c.target ? 1 : 0) | (c.src1 < c.target ? 2 : 0), 1)
+end
+
+"""
+    train_loss(m, x, auto_loss, cache, params, do_visualization=false)
+
+`train_loss` of src/training.jl:21-78 on the HIP path: returns `(loss, vis_disparity, vis_warped,
+vis_loss)` like the reference (`nothing`s when `do_visualization` is false).  The forward also
+runs the fused loss-tail pullback; the rrule below finishes the backward.
+"""
+function train_loss(m::HIPModel, x::ROCArray{Float32,5}, auto_loss, cache, params,
+                    do_visualization::Bool=false)
+    loss = ROCVector{Float32}(undef, 1)
+    check(ccall((:md2_model_forward_loss, lib), Cint,
+                (Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                m.handle, x, ptr(auto_loss), loss, C_NULL, stream_ptr()))
+    do_visualization || return (loss, nothing, nothing, nothing)
+    disps, pose = outputs(m)
+    cfg = loss_cfg(m); n = m.cfg.batch; c = m.cfg.in_channels; W = m.cfg.width; H = m.cfg.height
+    vis_loss = ROCArray{Float32}(undef, W, H, n, cfg.nscales)
+    vis_sel = ROCArray{Int8}(undef, W, H, n, cfg.nscales)
+    vis_warped = ROCArray{Float32}(undef, W, H, c, n, 2)
+    tmp = ROCVector{Float32}(undef, 1)
+    ws = ROCVector{UInt8}(undef, ccall((:md2_loss_workspace_size, lib), Csize_t, (Ref{LossCfg},), cfg))
+    out = LossOut(pointer(tmp), C_NULL, ntuple(_ -> Ptr{Float32}(C_NULL), 5), C_NULL,
+                  pointer(vis_loss), pointer(vis_sel), pointer(vis_warped))
+    dptrs = [pointer(d) for d in disps]
+    check(ccall((:md2_loss_fwd_bwd, lib), Cint,
+                (Ref{LossCfg}, Ptr{Ptr{Float32}}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Cfloat,
+                 Ref{LossOut}, Ptr{UInt8}, Ptr{Cvoid}),
+                cfg, dptrs, pose, x, ptr(auto_loss), 1f0, out, ws, stream_ptr()))
+    # training.jl:34-37,71-74: last disparity, both warped sources and the last scale's loss map
+    return (loss, disps[end], (vis_warped[:, :, :, :, 1], vis_warped[:, :, :, :, 2]),
+            reshape(vis_loss[:, :, :, end], W, H, 1, n))
+end
+
+# gradient(θ) do train_loss(...)[1] end: the remaining backward segments -> m.∇θ.  `bucket(off,
+# len)` runs after each segment (that flat range is final) so a DP caller can all-reduce it.
+function gradient!(m::HIPModel; bucket=(off, len) -> nothing)
+    nseg = ccall((:md2_model_num_segments, lib), Cint, (Ptr{Cvoid},), m.handle)
+    off, len = Ref{Clonglong}(), Ref{Clonglong}()
+    for k in 0:nseg-1
+        check(ccall((:md2_model_backward_segment, lib), Cint,
+                    (Ptr{Cvoid}, Cint, Ref{Clonglong}, Ref{Clonglong}, Ptr{Cvoid}),
+                    m.handle, k, off, len, stream_ptr()))
+        bucket(off[], len[])
+    end
+    return m.∇θ
+end
+
+# Zygote: d(train_loss(...)[1])/dθ.  The library's pullback is for dloss = 1; the scalar
+# cotangent scales it (the loss is a scalar, so that is the exact pullback).
+function ChainRulesCore.rrule(::typeof(train_loss), m::HIPModel, x, auto_loss, cache, params,
+                              do_visualization::Bool=false)
+    y = train_loss(m, x, auto_loss, cache, params, do_visualization)
+    function train_loss_pullback(Δ)
+        Δl = Δ[1] isa AbstractZero ? 0f0 : Float32(sum(Array(unthunk(Δ[1]))))
+        ∇ = gradient!(m)
+        Δl == 1f0 || (∇ .*= Δl)
+        return (NoTangent(), Tangent{HIPModel}(; θ=∇), NoTangent(), NoTangent(), NoTangent(),
+                NoTangent(), NoTangent())
+    end
+    return y, train_loss_pullback
+end
+
+# update!(ADAM(η), θ, ∇θ) -- Flux ADAM, β = (0.9, 0.999), ε = 1e-8 (scripts/script.jl:85)
+function update!(m::HIPModel, η; β=(0.9f0, 0.999f0), ϵ=1f-8, grad_scale=1f0)
+    m.step += 1
+    check(ccall((:md2_model_adam, lib), Cint,
+                (Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}, Cfloat, Cfloat, Cfloat, Cfloat, Cint, Cfloat, Ptr{Cvoid}),
+                m.handle, m.m, m.v, η, β[1], β[2], ϵ, m.step, grad_scale, stream_ptr()))
+end
+
+# eval_disparity(m, x) -- src/model.jl:63; x::(W,H,C,n), n <= batch
+function eval_disparity(m::HIPModel, x::ROCArray{Float32,4})
+    d = Vector{Ptr{Float32}}(undef, 5)
+    check(ccall((:md2_model_eval_disparity, lib), Cint,
+                (Ptr{Cvoid}, Ptr{Float32}, Cint, Ptr{Ptr{Float32}}, Ptr{Cvoid}),
+                m.handle, x, size(x, 4), d, stream_ptr()))
+    W, H = m.cfg.width, m.cfg.height; lv = m.cfg.scale_levels
+    return [unsafe_wrap(ROCArray, d[k], (W >> (5 - lv[k]), H >> (5 - lv[k]), 1, size(x, 4)))
+            for k in 1:m.cfg.n_levels]
+end
+
+# ------------------------------------------------------------------------------------------------
+# Op-level forward + rrule pairs (src/utils.jl, src/training.jl): for callers that keep Flux for
+# the networks and differentiate the loss ops one at a time.
+# ------------------------------------------------------------------------------------------------
+struct SSIM end                                        # src/utils.jl:17-43 (constants built in)
+
+function (s::SSIM)(x::ROCArray{Float32,4}, y::ROCArray{Float32,4})
+    W, H, C, N = size(x); out = similar(x)
+    check(ccall((:md2_ssim_fwd, lib), Cint,
+                (Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Ptr{Float32}, Ptr{Cvoid}),
+                x, y, N, C, H, W, out, stream_ptr()))
+    return out
+end
+
+function ChainRulesCore.rrule(s::SSIM, x::ROCArray{Float32,4}, y::ROCArray{Float32,4})
+    out = s(x, y)
+    function ssim_pullback(Δ)
+        W, H, C, N = size(x); dx = similar(x); dy = similar(y)
+        dout = ROCArray{Float32}(unthunk(Δ))
+        check(ccall((:md2_ssim_bwd, lib), Cint,
+                    (Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Ptr{Float32},
+                     Ptr{Float32}, Ptr{Cvoid}), x, y, dout, N, C, H, W, dx, dy, stream_ptr()))
+        return NoTangent(), dx, dy
+    end
+    return out, ssim_pullback
+end
+
+# Backproject: (b)(depth (1, W*H, N), invK) -> (3, W*H, N)   src/utils.jl:45-69
+struct Backproject; width::Int; height::Int; end
+function (b::Backproject)(depth::ROCArray{Float32,3}, invK)
+    N = size(depth, 3); out = ROCArray{Float32}(undef, 3, b.width * b.height, N)
+    iK = collect(rowmajor(invK))
+    check(ccall((:md2_backproject_fwd, lib), Cint,
+                (Ptr{Float32}, Cint, Cint, Cint, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                depth, N, b.width, b.height, iK, out, stream_ptr()))
+    return out
+end
+function ChainRulesCore.rrule(b::Backproject, depth::ROCArray{Float32,3}, invK)
+    out = b(depth, invK)
+    function backproject_pullback(Δ)
+        dd = similar(depth); dout = ROCArray{Float32}(unthunk(Δ)); iK = collect(rowmajor(invK))
+        check(ccall((:md2_backproject_bwd, lib), Cint,
+                    (Ptr{Float32}, Cint, Cint, Cint, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                    dout, size(depth, 3), b.width, b.height, iK, dd, stream_ptr()))
+        return NoTangent(), dd, NoTangent()            # invK: TrainCache constant
+    end
+    return out, backproject_pullback
+end
+
+# Project: (p)(points (3, W*H, N), K, R (3,3,N), t (3,1,N)) -> (2, W, H, N)   src/utils.jl:71-103
+struct Project; width::Int; height::Int; end
+rowmajor_batch(R) = ROCArray{Float32}(permutedims(Array(R), (2, 1, 3)))   # [n][3][3] row-major
+function (p::Project)(points::ROCArray{Float32,3}, K, R, t)
+    N = size(points, 3); out = ROCArray{Float32}(undef, 2, p.width, p.height, N)
+    check(ccall((:md2_project_fwd, lib), Cint,
+                (Ptr{Float32}, Cint, Cint, Cint, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                points, N, p.width, p.height, collect(rowmajor(K)), rowmajor_batch(R),
+                ROCArray{Float32}(t), out, stream_ptr()))
+    return out
+end
+function ChainRulesCore.rrule(p::Project, points::ROCArray{Float32,3}, K, R, t)
+    out = p(points, K, R, t)
+    function project_pullback(Δ)
+        N = size(points, 3); dpts = similar(points)
+        dRr = ROCArray{Float32}(undef, 9, N); dt = ROCArray{Float32}(undef, 3, 1, N)
+        ws = ROCVector{UInt8}(undef, ccall((:md2_project_workspace_size, lib), Csize_t,
+                                           (Cint, Cint, Cint), N, p.width, p.height))
+        check(ccall((:md2_project_bwd, lib), Cint,
+                    (Ptr{Float32}, Cint, Cint, Cint, Ptr{Float32}, Ptr{Float32}, Ptr{Float32},
+                     Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{UInt8}, Ptr{Cvoid}),
+                    points, N, p.width, p.height, collect(rowmajor(K)), rowmajor_batch(R),
+                    ROCArray{Float32}(t), ROCArray{Float32}(unthunk(Δ)), dpts, dRr, dt, ws, stream_ptr()))
+        dR = permutedims(reshape(dRr, 3, 3, N), (2, 1, 3))   # back to column-major (3,3,N)
+        return NoTangent(), dpts, NoTangent(), dR, dt
+    end
+    return out, project_pullback
+end
+
+# grid_sample(x, grid; padding_mode=:border), align_corners=true -- src/training.jl:56
+function grid_sample_border(x::ROCArray{Float32,4}, grid::ROCArray{Float32,4})
+    Wi, Hi, C, N = size(x); Wo, Ho = size(grid, 2), size(grid, 3)
+    out = ROCArray{Float32}(undef, Wo, Ho, C, N)
+    check(ccall((:md2_grid_sample_border_fwd, lib), Cint,
+                (Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Cint, Cint, Ptr{Float32}, Ptr{Cvoid}),
+                x, grid, N, C, Hi, Wi, Ho, Wo, out, stream_ptr()))
+    return out
+end
+function ChainRulesCore.rrule(::typeof(grid_sample_border), x::ROCArray{Float32,4}, grid::ROCArray{Float32,4})
+    out = grid_sample_border(x, grid)
+    function grid_sample_pullback(Δ)
+        Wi, Hi, C, N = size(x); Wo, Ho = size(grid, 2), size(grid, 3)
+        dgrid = similar(grid); dx = fill!(similar(x), 0)
+        check(ccall((:md2_grid_sample_border_bwd, lib), Cint,
+                    (Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Cint, Cint,
+                     Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                    x, grid, ROCArray{Float32}(unthunk(Δ)), N, C, Hi, Wi, Ho, Wo, dgrid, dx, stream_ptr()))
+        return NoTangent(), dx, dgrid
+    end
+    return out, grid_sample_pullback
+end
+
+# smooth_loss(disparity (W,H,N), image (W,H,C,N)) -> scalar   src/utils.jl:163-177
+function smooth_loss(disp::ROCArray{Float32}, img::ROCArray{Float32,4})
+    W, H, C, N = size(img); loss = ROCVector{Float32}(undef, 1)
+    ws = ROCVector{UInt8}(undef, ccall((:md2_smooth_loss_workspace_size, lib), Csize_t, (Cint, Cint, Cint), N, W, H))
+    check(ccall((:md2_smooth_loss_fwd, lib), Cint,
+                (Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Ptr{Float32}, Ptr{UInt8}, Ptr{Cvoid}),
+                disp, img, N, C, H, W, loss, ws, stream_ptr()))
+    return Array(loss)[1]
+end
+function ChainRulesCore.rrule(::typeof(smooth_loss), disp::ROCArray{Float32}, img::ROCArray{Float32,4})
+    l = smooth_loss(disp, img)
+    function smooth_loss_pullback(Δ)
+        W, H, C, N = size(img); dd = similar(disp)
+        ws = ROCVector{UInt8}(undef, ccall((:md2_smooth_loss_workspace_size, lib), Csize_t, (Cint, Cint, Cint), N, W, H))
+        check(ccall((:md2_smooth_loss_bwd, lib), Cint,
+                    (Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Cfloat, Ptr{Float32}, Ptr{UInt8}, Ptr{Cvoid}),
+                    disp, img, N, C, H, W, Float32(unthunk(Δ)), dd, ws, stream_ptr()))
+        return NoTangent(), dd, NoTangent()
+    end
+    return l, smooth_loss_pullback
+end
+
+# One scale of train_loss's loop body (src/training.jl:43-62): upsample -> depth -> Backproject ->
+# Project -> grid_sample -> photometric_loss -> min over sources [-> _apply_mask].
+# disp (dw,dh,1,N); Rt (12, N, 2) = composeT outputs (R row-major, t); x (W,H,C,3,N).
+function warp_photometric(cfg::WarpCfg, disp, Rt, x, automask=nothing)
+    loss = ROCArray{Float32}(undef, cfg.width, cfg.height, 1, cfg.n)
+    ws = ROCVector{UInt8}(undef, ccall((:md2_warp_photometric_workspace_size, lib), Csize_t, (Ref{WarpCfg},), cfg))
+    check(ccall((:md2_warp_photometric_fwd, lib), Cint,
+                (Ref{WarpCfg}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32},
+                 Ptr{Int8}, Ptr{UInt8}, Ptr{Cvoid}),
+                cfg, disp, Rt, x, ptr(automask), loss, C_NULL, ws, stream_ptr()))
+    return loss
+end
+function ChainRulesCore.rrule(::typeof(warp_photometric), cfg::WarpCfg, disp, Rt, x, automask=nothing)
+    loss = warp_photometric(cfg, disp, Rt, x, automask)
+    function warp_photometric_pullback(Δ)
+        dd = similar(disp); dRt = similar(Rt)
+        ws = ROCVector{UInt8}(undef, ccall((:md2_warp_photometric_workspace_size, lib), Csize_t, (Ref{WarpCfg},), cfg))
+        check(ccall((:md2_warp_photometric_bwd, lib), Cint,
+                    (Ref{WarpCfg}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32},
+                     Ptr{Float32}, Ptr{Float32}, Ptr{UInt8}, Ptr{Cvoid}),
+                    cfg, disp, Rt, x, ptr(automask), ROCArray{Float32}(unthunk(Δ)), dd, dRt, ws, stream_ptr()))
+        return NoTangent(), NoTangent(), dd, dRt, NoTangent(), NoTangent()
+    end
+    return loss, warp_photometric_pullback
+end
+
+# composeT(so3_exp_map(rvec), tvec, invert) for the 2n poses (src/utils.jl:106-145,185-192);
+# pose (6, 2n) = (rvec, tvec) per (source, sample); bit s of invert_mask: source s < target.
+function so3_compose(pose::ROCArray{Float32,2}, invert_mask::Integer)
+    n = size(pose, 2) ÷ 2; Rt = ROCArray{Float32}(undef, 12, 2n)
+    check(ccall((:md2_so3_compose_fwd, lib), Cint, (Ptr{Float32}, Cint, Cint, Ptr{Float32}, Ptr{Cvoid}),
+                pose, n, invert_mask, Rt, stream_ptr()))
+    return Rt
+end
+function ChainRulesCore.rrule(::typeof(so3_compose), pose::ROCArray{Float32,2}, invert_mask::Integer)
+    Rt = so3_compose(pose, invert_mask)
+    function so3_compose_pullback(Δ)
+        dpose = similar(pose)
+        check(ccall((:md2_so3_compose_bwd, lib), Cint,
+                    (Ptr{Float32}, Cint, Cint, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                    pose, size(pose, 2) ÷ 2, invert_mask, ROCArray{Float32}(unthunk(Δ)), dpose, stream_ptr()))
+        return NoTangent(), dpose, NoTangent()
+    end
+    return Rt, so3_compose_pullback
+end
+
+# ------------------------------------------------------------------------------------------------
+# Data parallel: one Julia process per GPU over the library's own RCCL communicator (SURVEY 8e;
+# the reference's loop is scripts/script.jl:84-86).  Rank 0 writes the unique id to `idfile`.
+# ------------------------------------------------------------------------------------------------
+function comm_init(rank, nranks, device, idfile)
+    id = zeros(UInt8, 128)
+    if rank == 0
+        check(ccall((:md2_comm_get_unique_id, lib), Cint, (Ptr{UInt8},), id))
+        write(idfile * ".tmp", id); mv(idfile * ".tmp", idfile; force=true)
+    else
+        while !isfile(idfile); sleep(0.05); end
+        id .= read(idfile)
+    end
+    c = Ref{Ptr{Cvoid}}()
+    check(ccall((:md2_comm_init, lib), Cint, (Cint, Cint, Ptr{UInt8}, Cint, Ref{Ptr{Cvoid}}),
+                rank, nranks, id, device, c))
+    return c[]
+end
+
+# forward + loss + backward with each bucket's RCCL all-reduce overlapped + ADAM (1/nranks)
+function train_step_dp!(m::HIPModel, comm::Ptr{Cvoid}, x, auto_loss, η; β=(0.9f0, 0.999f0), ϵ=1f-8)
+    m.step += 1; loss = ROCVector{Float32}(undef, 1)
+    check(ccall((:md2_model_train_step_dp, lib), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32},
+                 Cfloat, Cfloat, Cfloat, Cfloat, Cint, Ptr{Float32}, Ptr{Cvoid}),
+                m.handle, comm, x, ptr(auto_loss), m.m, m.v, η, β[1], β[2], ϵ, m.step, loss, stream_ptr()))
+    return loss
+end
+
+end # module

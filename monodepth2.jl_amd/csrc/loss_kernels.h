@@ -16,10 +16,21 @@ struct Geom {
   int W, H;          // full (target) resolution
 };
 
-struct PhotoArgs {
+// One scale of the photometric pass: its disparity (any resolution <= the target's, upsampled
+// in-kernel with align_corners) and its outputs.
+struct PhotoScale {
   const float* disp;      // [N][dh][dw]  (sigmoid output of one scale)
   int dw, dh;
   float rx, ry;           // (dw-1)/(W-1), (dh-1)/(H-1)  align_corners upsample ratios
+  float* g_disp;          // [N][H][W] out: d loss / d full-res disparity (store)
+  float* partials;        // [N*tiles][25]: loss sum, dR0(9) dt0(3), dR1(9) dt1(3)
+  float* loss_map;        // [N][H][W] per-pixel warp loss (train_loss vis_loss) or nullptr
+  signed char* sel_map;   // [N][H][W] chosen source (0/1, -1 = automask) or nullptr
+};
+
+struct PhotoArgs {
+  PhotoScale sc[MAX_SCALES];
+  int nscales;
   const float* x;         // frames
   long x_sample_stride;   // elements between samples
   long x_frame_stride;    // elements between frames of a sample
@@ -28,12 +39,16 @@ struct PhotoArgs {
   const float* automask;  // [N][H][W] identity-reprojection loss or nullptr
   float wloss;            // d(total loss) / d(per-pixel warp loss)
   const float* gmap;      // [N][H][W] per-pixel cotangent (times wloss) or nullptr (uniform)
-  float* g_disp;          // [N][H][W] out: d loss / d full-res disparity (store)
-  float* partials;        // [blocks][25]: loss sum, dR0(9) dt0(3), dR1(9) dt1(3)
-  float* loss_map;        // [N][H][W] per-pixel warp loss (train_loss vis_loss) or nullptr
-  signed char* sel_map;   // [N][H][W] chosen source (0/1, -1 = automask) or nullptr
   int N;
 };
+
+// Wave tiling of the photometric pass (photo.hip): 60 output columns x `rows` output rows per
+// wave, tiles_x * tiles_y tiles per sample and scale.
+struct PhotoTiling {
+  int tiles_x, tiles_y, rows;
+  long per_scale() const { return (long)tiles_x * tiles_y; }
+};
+PhotoTiling photo_tiling(int W, int H, int N, int nscales);
 
 struct SmoothArgs {
   const float* disp;
@@ -78,14 +93,16 @@ struct FinalizeArgs {
   int N;
 };
 
+// all a.nscales scales in one launch (photo.hip)
 int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st);
 // identity-reprojection loss (training.jl:9-11): out [N][H][W] = min over the two raw sources of
 // photometric_loss(source, target)
 int launch_automask(const float* x, long x_sample_stride, long x_frame_stride, int target,
                     int src0, int src1, int N, int C, int H, int W, float* out, hipStream_t st);
 // warped sources only (train_loss vis_warped): out [2][N][C][H][W]
-int launch_warp_vis(const PhotoArgs& a, const Geom& g, int C, float* out, hipStream_t st);
-long photometric_blocks(int W, int H, int N);
+int launch_warp_vis(const PhotoArgs& a, int scale, const Geom& g, int C, float* out, hipStream_t st);
+// partial rows per scale of the photometric pass run with `nscales` scales
+long photometric_blocks(int W, int H, int N, int nscales);
 long smooth_blocks(int W, int H, int N);
 int launch_disp_sum(const float* disp, int dw, int dh, float rx, float ry, int W, int H, int N,
                     int parts, float* out, hipStream_t st);

@@ -1,20 +1,12 @@
-// Photometric loss tail of the Monodepth2.jl train step, fused forward+backward (gfx950).
+// Loss-tail kernels of the Monodepth2.jl train step around the photometric pass (photo.hip):
+// disparity means, edge-aware smoothness, the upsample adjoint, final reductions, so3/composeT,
+// and the visualisation warp (gfx950).
 //
-// Reference: src/training.jl:21-78 (train_loss), :1-19 (photometric / prediction / automask),
-// src/utils.jl:17-43 (SSIM), :45-103 (Backproject / Project / normalize), :106-145 (so3 + hat),
+// Reference: src/training.jl:21-78 (train_loss), src/utils.jl:106-145 (so3 + hat),
 // :163-183 (smooth_loss, disparity_to_depth), :185-192 (composeT).
-//
-// The loss is a pixel MEAN of terminal per-pixel terms, so its gradient w.r.t. every per-pixel
-// term is a known constant: one pass per scale computes the forward value AND the backward
-// (d disparity, d R, d t) with no saved activations.  Per scale and pixel the kernel reads the
-// disparity, the target and two sources (bilinear gathers) and writes one gradient float.
 #include "loss_kernels.h"
 
 namespace md2 {
-
-__device__ __forceinline__ int reflect_idx(int i, int n) {
-  return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
-}
 
 // Bilinear align_corners=true upsample of one value (NNlib upsample_bilinear(x; size)),
 // src/training.jl:45.  ratio = (in-1)/(out-1).
@@ -35,19 +27,6 @@ __device__ __forceinline__ float disp_at(const float* __restrict__ d, int dw, in
                                          float ry, int W, int H, int X, int Y) {
   if (dw == W && dh == H) return d[Y * W + X];
   return upsample_at(d, dw, dh, rx, ry, X, Y);
-}
-
-// disp_at through a buffer resource (32-bit offsets: no 64-bit address per load)
-__device__ __forceinline__ float disp_at_b(__amdgpu_buffer_rsrc_t r, int dw, int dh, float rx,
-                                           float ry, int W, int H, int X, int Y) {
-  if (dw == W && dh == H) return bload(r, (uint32_t)(Y * W + X) * 4u);
-  const float sx = rx * (float)X, sy = ry * (float)Y;
-  const int ix0 = min((int)sx, dw - 1), iy0 = min((int)sy, dh - 1);
-  const int ix1 = min(ix0 + 1, dw - 1), iy1 = min(iy0 + 1, dh - 1);
-  const float fx = sx - (float)ix0, fy = sy - (float)iy0;
-  const float v00 = bload(r, (uint32_t)(iy0 * dw + ix0) * 4u), v01 = bload(r, (uint32_t)(iy0 * dw + ix1) * 4u);
-  const float v10 = bload(r, (uint32_t)(iy1 * dw + ix0) * 4u), v11 = bload(r, (uint32_t)(iy1 * dw + ix1) * 4u);
-  return (1.f - fy) * ((1.f - fx) * v00 + fx * v01) + fy * ((1.f - fx) * v10 + fx * v11);
 }
 
 struct Proj {
@@ -79,423 +58,12 @@ __device__ __forceinline__ void project_point(const Geom& g, const float* Rt, fl
   p.iy = ((gy + 1.f) * 0.5f) * g.hm1;
 }
 
-// Back-propagate d(ix, iy) of one source through normalize/Project/Backproject:
-// accumulates dR (9), dt (3) and returns d(depth).
-__device__ __forceinline__ float project_point_grad(const Geom& g, const float* Rt,
-                                                    const Proj& p, float dix, float diy,
-                                                    float ray0, float ray1, float ray2,
-                                                    float* dRt) {
-  // ix = ((gx+1)/2) (W-1),  gx = ((u-1)/(W-1) - 1/2) 2
-  const float du = dix * (g.wm1 * 0.5f) * (2.f / g.wm1);
-  const float dv = diy * (g.hm1 * 0.5f) * (2.f / g.hm1);
-  float dcam[3];
-  dcam[0] = du * p.denom;
-  dcam[1] = dv * p.denom;
-  dcam[2] = -(du * p.cam[0] + dv * p.cam[1]) * p.denom * p.denom;
-  float dP[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) dP[j] = g.K[j] * dcam[0] + g.K[3 + j] * dcam[1] + g.K[6 + j] * dcam[2];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) dRt[3 * i + j] += dP[i] * p.X[j];
-    dRt[9 + i] += dP[i];
-  }
-  float dX[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) dX[j] = Rt[j] * dP[0] + Rt[3 + j] * dP[1] + Rt[6 + j] * dP[2];
-  return dX[0] * ray0 + dX[1] * ray1 + dX[2] * ray2;
-}
-
 __device__ __forceinline__ void ray_at(const Geom& g, int gx, int gy, float& r0, float& r1,
                                        float& r2) {
   const float w = (float)(gx + 1), h = (float)(gy + 1);   // 1-based grid (src/utils.jl:51-55)
   r0 = g.invK[0] * w + g.invK[1] * h + g.invK[2];
   r1 = g.invK[3] * w + g.invK[4] * h + g.invK[5];
   r2 = g.invK[6] * w + g.invK[7] * h + g.invK[8];
-}
-
-// Bilinear sample of C channels at a border-clamped coordinate and, for the backward, its
-// derivative terms: d sample_c / d ix = mx * Gx[c], d sample_c / d iy = my * Gy[c] (corners
-// outside the image contribute zero; mx, my are the border-clip masks).  Straight-line: the
-// out-of-range corners are read at a clamped address and weighted / selected away.
-template <int C, bool GRAD>
-__device__ __forceinline__ void sample_vg(__amdgpu_buffer_rsrc_t rs, uint32_t soff, uint32_t HW4,
-                                          int W, int H, float ix, float iy, float (&out)[C],
-                                          float (&Gx)[C], float (&Gy)[C], float& mx, float& my) {
-  const float x = fminf(fmaxf(ix, 0.f), (float)(W - 1));
-  const float y = fminf(fmaxf(iy, 0.f), (float)(H - 1));
-  const int x0 = (int)x, y0 = (int)y;
-  const bool okx = x0 + 1 < W, oky = y0 + 1 < H;
-  const int x1 = okx ? x0 + 1 : x0, y1 = oky ? y0 + 1 : y0;
-  const float fx = x - (float)x0, fy = y - (float)y0;
-  const float w00 = (1.f - fx) * (1.f - fy), w01 = fx * (1.f - fy);
-  const float w10 = (1.f - fx) * fy, w11 = fx * fy;
-  const uint32_t o00 = (uint32_t)(y0 * W + x0) * 4u, o01 = (uint32_t)(y0 * W + x1) * 4u;
-  const uint32_t o10 = (uint32_t)(y1 * W + x0) * 4u, o11 = (uint32_t)(y1 * W + x1) * 4u;
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const uint32_t so = soff + (uint32_t)c * HW4;
-    const float v00 = bload_s(rs, o00, so), v01 = bload_s(rs, o01, so);
-    const float v10 = bload_s(rs, o10, so), v11 = bload_s(rs, o11, so);
-    float v = w00 * v00;
-    v += okx ? w01 * v01 : 0.f;
-    v += oky ? w10 * v10 : 0.f;
-    v += (okx && oky) ? w11 * v11 : 0.f;
-    out[c] = v;
-    if (GRAD) {
-      const float u01 = okx ? v01 : 0.f, u10 = oky ? v10 : 0.f, u11 = (okx && oky) ? v11 : 0.f;
-      Gx[c] = (u01 - v00) * (1.f - fy) + (u11 - u10) * fy;
-      Gy[c] = (u10 - v00) * (1.f - fx) + (u11 - u01) * fx;
-    }
-  }
-  if (GRAD) {
-    mx = (ix > 0.f && ix < (float)(W - 1)) ? 1.f : 0.f;
-    my = (iy > 0.f && iy < (float)(H - 1)) ? 1.f : 0.f;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Fused warp + SSIM + L1 + min-over-sources (+ automask) forward and backward, one scale.
-// Tile PT_W x PT_H output pixels per 256-thread block, one centre pixel per thread.
-//  phase 1  warps of both sources + target on the halo-2 region: every thread its centre pixel
-//           (keeping that pixel's projection and bilinear-derivative terms in registers for the
-//           backward), the first RA threads one pixel of the halo ring;
-//  phase 2  SSIM + L1 per source on the halo-1 region (centre + ring item), min over sources,
-//           adjoint coefficients into LDS;
-//  phase 3  adjoint of the 3x3 reflect windows at the centre, geometry backward from registers.
-// ---------------------------------------------------------------------------------------------
-constexpr int PT_W = 32, PT_H = 8;
-
-// coordinates (in the (TW+2h) x (TH+2h) region) of ring pixel r of the h-wide halo
-template <int TW, int TH, int HALO>
-__device__ __forceinline__ void ring_xy(int r, int& rx, int& ry) {
-  constexpr int RW = TW + 2 * HALO;
-  constexpr int TOP = HALO * RW;
-  if (r < TOP) { rx = r % RW; ry = r / RW; return; }
-  r -= TOP;
-  if (r < TOP) { rx = r % RW; ry = TH + HALO + r / RW; return; }
-  r -= TOP;                                 // side columns: HALO left + HALO right per row
-  const int row = r / (2 * HALO), k = r % (2 * HALO);
-  ry = HALO + row;
-  rx = k < HALO ? k : TW + k;
-}
-
-#ifdef MD2_PHOTO_WPE
-#define MD2_PHOTO_ATTR __attribute__((amdgpu_waves_per_eu(MD2_PHOTO_WPE, 8)))
-#else
-#define MD2_PHOTO_ATTR
-#endif
-template <int C>
-__global__ __launch_bounds__(256) MD2_PHOTO_ATTR void photometric_kernel(PhotoArgs a, Geom g) {
-  constexpr int AW = PT_W + 4, AH = PT_H + 4, NA = AW * AH;
-  constexpr int BW = PT_W + 2, BH = PT_H + 2, NB = BW * BH;
-  constexpr int NT = PT_W * PT_H;
-  constexpr int RA = NA - NT, RB = NB - NT;
-  static_assert(NT == 256 && RA <= 256 && RB <= 256, "tile / ring sizes");
-  // per halo-1 pixel and channel: SSIM partials w.r.t. (mu_x, var_x, cov_xy) of the selected
-  // source and the window means mu_x, mu_y -- the adjoint is evaluated in the centred form
-  // g_m + 2 g_v (x_q - mu_x) + g_c (y_q - mu_y) (no E[x^2] - E[x]^2 cancellation in fp32).
-  constexpr int NCOEF = 5;                  // g_m, g_v, g_c, mu_x, mu_y
-  constexpr int IMG = 3 * C * NA;           // x[2][C][NA], y[C][NA]      (phases 1-2)
-  constexpr int COEF = NCOEF * C * NB;      // coef[NCOEF*C][NB]          (phases 2-3)
-  __shared__ float s_buf[IMG + COEF];
-  __shared__ int s_sel[NB];
-  __shared__ float s_red[4 * 25];
-#define SX(s, c, i) s_buf[((s) * C + (c)) * NA + (i)]
-#define SY(c, i) s_buf[(2 * C + (c)) * NA + (i)]
-#define SC(k, i) s_buf[IMG + (k) * NB + (i)]
-
-  const int W = g.W, H = g.H;
-  const long HW = (long)W * H;
-  const int n = blockIdx.z;
-  const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
-  // one buffer resource per sample (frames and channels by wave-uniform soffset), one for the
-  // sample's disparity map
-  const __amdgpu_buffer_rsrc_t rxs =
-      make_rsrc(a.x + (long)n * a.x_sample_stride, (uint32_t)(a.x_sample_stride * 4));
-  const __amdgpu_buffer_rsrc_t rdsp =
-      make_rsrc(a.disp + (long)n * a.dw * a.dh, (uint32_t)a.dw * a.dh * 4u);
-  const uint32_t HW4 = (uint32_t)HW * 4u;
-  const uint32_t so_t = (uint32_t)(a.target * a.x_frame_stride * 4);
-  const uint32_t so_s[2] = {(uint32_t)(a.src0 * a.x_frame_stride * 4),
-                            (uint32_t)(a.src1 * a.x_frame_stride * 4)};
-  float Rt0[12], Rt1[12];
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    Rt0[i] = a.Rt[(long)n * 12 + i];
-    Rt1[i] = a.Rt[(long)(a.N + n) * 12 + i];
-  }
-  const int t = threadIdx.x;
-  const int tx = t % PT_W, ty = t / PT_W;
-  const int cgx = x0 + tx, cgy = y0 + ty;                 // centre pixel
-  const bool cvalid = cgx < W && cgy < H;
-
-  // ---- phase 1 ------------------------------------------------------------------------------
-  // centre state kept for phase 3
-  // (the centre's warped / target values stay in the LDS tiles; its projection is recomputed)
-  float Gx[2][C], Gy[2][C], depth_c;
-  {
-    int rax = 0, ray = 0;
-    if (t < RA) ring_xy<PT_W, PT_H, 2>(t, rax, ray);
-    const int rgx = x0 - 2 + rax, rgy = y0 - 2 + ray;
-    const bool rvalid = t < RA && rgx >= 0 && rgx < W && rgy >= 0 && rgy < H;
-    // clamped coordinates: every load below is in bounds, only the LDS stores are predicated
-    const int gxs[2] = {min(cgx, W - 1), min(max(rgx, 0), W - 1)};
-    const int gys[2] = {min(cgy, H - 1), min(max(rgy, 0), H - 1)};
-    float dv[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) dv[k] = disp_at_b(rdsp, a.dw, a.dh, a.rx, a.ry, W, H, gxs[k], gys[k]);
-    float yv[2][C];
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-        yv[k][c] = bload_s(rxs, (uint32_t)(gys[k] * W + gxs[k]) * 4u, so_t + (uint32_t)c * HW4);
-    float wv[2][2][C];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const float depth = 1.f / (dv[k] * g.disp_range + g.min_disp);
-      float r0, r1, r2;
-      ray_at(g, gxs[k], gys[k], r0, r1, r2);
-      if (k == 0) depth_c = depth;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        Proj p;
-        project_point(g, s ? Rt1 : Rt0, depth, r0, r1, r2, p);
-        if (k == 0) {
-          float mdx, mdy;
-          sample_vg<C, true>(rxs, so_s[s], HW4, W, H, p.ix, p.iy, wv[k][s], Gx[s], Gy[s], mdx, mdy);
-        } else {
-          float gdx[C], gdy[C], mdx, mdy;
-          sample_vg<C, false>(rxs, so_s[s], HW4, W, H, p.ix, p.iy, wv[k][s], gdx, gdy, mdx, mdy);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);   // one item's gathers in flight: fewer live VGPRs
-    }
-    if (cvalid) {
-      const int i = (ty + 2) * AW + tx + 2;
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        SX(0, c, i) = wv[0][0][c];
-        SX(1, c, i) = wv[0][1][c];
-        SY(c, i) = yv[0][c];
-      }
-    }
-    if (rvalid) {
-      const int i = ray * AW + rax;
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        SX(0, c, i) = wv[1][0][c];
-        SX(1, c, i) = wv[1][1][c];
-        SY(c, i) = yv[1][c];
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 2 ------------------------------------------------------------------------------
-  const float kS = a.wloss * 0.85f / (float)C * (1.f / 9.f);
-  const float c1 = 1e-4f, c2 = 9e-4f;
-  const float ninth = 1.f / 9.f;
-  float thread_loss = 0.f;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    int bx, by;
-    if (k == 0) {
-      bx = tx + 1;
-      by = ty + 1;
-    } else {
-      bx = 0;
-      by = 0;
-      if (t < RB) ring_xy<PT_W, PT_H, 1>(t, bx, by);
-    }
-    const int gx = x0 - 1 + bx, gy = y0 - 1 + by;
-    const bool live = (k == 0 || t < RB) && gx >= 0 && gx < W && gy >= 0 && gy < H;
-    const int bi = by * BW + bx;
-    if (!live) continue;
-    int wi[9];
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int ax = reflect_idx(gx + dx, W) - (x0 - 2);
-        const int ay = reflect_idx(gy + dy, H) - (y0 - 2);
-        wi[(dy + 1) * 3 + dx + 1] = ay * AW + ax;
-      }
-    const int ci = (by + 1) * AW + (bx + 1);     // centre in region A
-    // per-pixel cotangent of this window centre's loss (op-level pullback; 1 in train_loss)
-    const float gp = a.gmap ? a.gmap[((long)n * H + gy) * W + gx] : 1.f;
-    float loss_s[2] = {0.f, 0.f};
-    float coef1[NCOEF * C];                   // source 1 (source 0 goes straight to LDS)
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      // window moments shifted by the centre value (exact algebra, better fp32 conditioning)
-      const float yc = SY(c, ci);
-      float yw[9];
-      float sy = 0.f, syy = 0.f;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) {
-        yw[q] = SY(c, wi[q]) - yc;
-        sy += yw[q];
-        syy += yw[q] * yw[q];
-      }
-      const float eyd = sy * ninth;
-      const float my = yc + eyd, vy = syy * ninth - eyd * eyd;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const float xc = SX(s, c, ci);
-        float sx = 0.f, sxx = 0.f, sxy = 0.f;
-#pragma unroll
-        for (int q = 0; q < 9; ++q) {
-          const float dx = SX(s, c, wi[q]) - xc;
-          sx += dx;
-          sxx += dx * dx;
-          sxy += dx * yw[q];
-        }
-        const float exd = sx * ninth;
-        const float mx = xc + exd;
-        const float vx = sxx * ninth - exd * exd, cxy = sxy * ninth - exd * eyd;
-        const float A1 = 2.f * mx * my + c1, A2 = 2.f * cxy + c2;
-        const float B1 = mx * mx + my * my + c1, B2 = vx + vy + c2;
-        const float num = A1 * A2, den_ = B1 * B2;
-        const float val = (1.f - num / den_) * 0.5f;
-        const float sv = fminf(fmaxf(val, 0.f), 1.f);
-        loss_s[s] += 0.85f / (float)C * sv + 0.15f / (float)C * fabsf(yc - xc);
-        const float lv = (val >= 0.f && val <= 1.f) ? 1.f : 0.f;
-        const float dn = -0.5f / den_ * lv, dd = 0.5f * num / (den_ * den_) * lv;
-        const float kp = kS * gp;
-        const float cq[NCOEF] = {kp * (dn * 2.f * my * A2 + dd * 2.f * mx * B2),  // d/d mu_x
-                                 kp * dd * B1,                                    // d/d var_x
-                                 kp * dn * 2.f * A1,                              // d/d cov_xy
-                                 mx, my};
-#pragma unroll
-        for (int q = 0; q < NCOEF; ++q) {
-          if (s == 0)
-            SC(NCOEF * c + q, bi) = cq[q];
-          else
-            coef1[NCOEF * c + q] = cq[q];
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);   // bound the hoisted window reads to one channel
-    }
-    // minimum over sources (first argmin), then optional automask (mask first => wins ties)
-    int sel = (loss_s[1] < loss_s[0]) ? 1 : 0;
-    float lmin = sel ? loss_s[1] : loss_s[0];
-    if (a.automask) {
-      const float am = a.automask[((long)n * H + gy) * W + gx];
-      if (!(lmin < am)) {
-        sel = -1;
-        lmin = am;
-      }
-    }
-    s_sel[bi] = sel;
-    if (sel == 1) {
-#pragma unroll
-      for (int q = 0; q < NCOEF * C; ++q) SC(q, bi) = coef1[q];
-    }
-    if (k == 0) {
-      thread_loss = lmin;
-      const long qq = ((long)n * H + gy) * W + gx;
-      if (a.loss_map) a.loss_map[qq] = lmin;
-      if (a.sel_map) a.sel_map[qq] = (signed char)sel;
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 3 ------------------------------------------------------------------------------
-  float acc[25];
-#pragma unroll
-  for (int k = 0; k < 25; ++k) acc[k] = 0.f;
-  acc[0] = thread_loss;
-  if (cvalid) {
-    const int gx = cgx, gy = cgy;
-    float xq[2][C], yq[C];
-    {
-      const int ai = (ty + 2) * AW + tx + 2;
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        xq[0][c] = SX(0, c, ai);
-        xq[1][c] = SX(1, c, ai);
-        yq[c] = SY(c, ai);
-      }
-    }
-    float dxs[2][C];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int c = 0; c < C; ++c) dxs[s][c] = 0.f;
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int py = gy + dy;
-      if (py < 0 || py >= H) continue;
-      const float wy = 1.f + ((gy == 1 && py == 0) ? 1.f : 0.f) + ((gy == H - 2 && py == H - 1) ? 1.f : 0.f);
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int px = gx + dx;
-        if (px < 0 || px >= W) continue;
-        const float wx = 1.f + ((gx == 1 && px == 0) ? 1.f : 0.f) + ((gx == W - 2 && px == W - 1) ? 1.f : 0.f);
-        const int bi = (py - (y0 - 1)) * BW + (px - (x0 - 1));
-        const int sel = s_sel[bi];
-        if (sel < 0) continue;
-        const float w = wx * wy;
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const float xv = sel ? xq[1][c] : xq[0][c];
-          const float tt = SC(NCOEF * c + 0, bi) +
-                           2.f * SC(NCOEF * c + 1, bi) * (xv - SC(NCOEF * c + 3, bi)) +
-                           SC(NCOEF * c + 2, bi) * (yq[c] - SC(NCOEF * c + 4, bi));
-          if (sel)
-            dxs[1][c] += w * tt;
-          else
-            dxs[0][c] += w * tt;
-        }
-        __builtin_amdgcn_sched_barrier(0);   // one neighbour's coefficients in flight at a time
-      }
-    }
-    const int selq = s_sel[(ty + 1) * BW + (tx + 1)];
-    const float kL = a.wloss * 0.15f / (float)C * (a.gmap ? a.gmap[((long)n * H + gy) * W + gx] : 1.f);
-    float ddepth = 0.f;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bool any = false;
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        if (selq == s) {
-          const float df = xq[s][c] - yq[c];   // d|y - x|/dx = sign(x - y), abs'(0) = 0
-          dxs[s][c] += kL * (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f));
-        }
-        any = any || (dxs[s][c] != 0.f);
-      }
-      if (!any) continue;
-      float gxs = 0.f, gys = 0.f;
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        gxs += dxs[s][c] * Gx[s][c];
-        gys += dxs[s][c] * Gy[s][c];
-      }
-      float r0, r1, r2;
-      ray_at(g, gx, gy, r0, r1, r2);
-      Proj p;
-      project_point(g, s ? Rt1 : Rt0, depth_c, r0, r1, r2, p);
-      // border-clip masks of the sample coordinate (clip_coordinates_set_grad)
-      const float mx = (p.ix > 0.f && p.ix < (float)(W - 1)) ? 1.f : 0.f;
-      const float my = (p.iy > 0.f && p.iy < (float)(H - 1)) ? 1.f : 0.f;
-      ddepth += project_point_grad(g, s ? Rt1 : Rt0, p, gxs * mx, gys * my, r0, r1, r2,
-                                   &acc[1 + 12 * s]);
-    }
-    // depth = 1/(disp*range + min_disp)  =>  d depth/d disp = -range * depth^2
-    a.g_disp[((long)n * H + gy) * W + gx] = -ddepth * g.disp_range * depth_c * depth_c;
-  }
-  block_sum256<25>(acc, s_red);
-  if (threadIdx.x == 0) {
-    const long blk = ((long)n * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-#pragma unroll
-    for (int k = 0; k < 25; ++k) a.partials[blk * 25 + k] = acc[k];
-  }
-#undef SX
-#undef SY
-#undef SC
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -879,31 +447,18 @@ __global__ void so3_bwd_kernel(const float* __restrict__ pose, int count, int N,
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
-int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st) {
-  dim3 grid(cdiv(g.W, PT_W), cdiv(g.H, PT_H), a.N);
-  if (C == 3)
-    hipLaunchKernelGGL(photometric_kernel<3>, grid, dim3(256), 0, st, a, g);
-  else if (C == 1)
-    hipLaunchKernelGGL(photometric_kernel<1>, grid, dim3(256), 0, st, a, g);
-  else {
-    set_error("photometric: channels must be 1 or 3");
-    return MD2_ENOTSUP;
-  }
-  MD2_LAUNCH_CHECK();
-  return MD2_OK;
-}
-
 // Visualisation warp (train_loss vis_warped, src/training.jl:48-57,71-73): both sources
 // resampled through the scale's depth and pose, no loss, no backward.  One thread per target
 // pixel, all C channels of both sources; same geometry helpers as the photometric kernel.
 template <int C>
-__global__ __launch_bounds__(256) void warp_vis_kernel(PhotoArgs a, Geom g, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void warp_vis_kernel(PhotoArgs a, int scale, Geom g, float* __restrict__ out) {
+  const PhotoScale sc = a.sc[scale];
   const int HW = g.W * g.H;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long)a.N * HW) return;
   const int n = (int)(idx / HW), pix = (int)(idx - (long)n * HW);
   const int Y = pix / g.W, X = pix - Y * g.W;
-  const float d = disp_at(a.disp + (long)n * a.dw * a.dh, a.dw, a.dh, a.rx, a.ry, g.W, g.H, X, Y);
+  const float d = disp_at(sc.disp + (long)n * sc.dw * sc.dh, sc.dw, sc.dh, sc.rx, sc.ry, g.W, g.H, X, Y);
   const float depth = 1.f / (d * g.disp_range + g.min_disp);
   float r0, r1, r2;
   ray_at(g, X, Y, r0, r1, r2);
@@ -928,13 +483,13 @@ __global__ __launch_bounds__(256) void warp_vis_kernel(PhotoArgs a, Geom g, floa
   }
 }
 
-int launch_warp_vis(const PhotoArgs& a, const Geom& g, int C, float* out, hipStream_t st) {
+int launch_warp_vis(const PhotoArgs& a, int scale, const Geom& g, int C, float* out, hipStream_t st) {
   const long n = (long)a.N * g.W * g.H;
   const dim3 grid((unsigned)cdiv(n, 256L));
   if (C == 3)
-    hipLaunchKernelGGL(warp_vis_kernel<3>, grid, dim3(256), 0, st, a, g, out);
+    hipLaunchKernelGGL(warp_vis_kernel<3>, grid, dim3(256), 0, st, a, scale, g, out);
   else if (C == 1)
-    hipLaunchKernelGGL(warp_vis_kernel<1>, grid, dim3(256), 0, st, a, g, out);
+    hipLaunchKernelGGL(warp_vis_kernel<1>, grid, dim3(256), 0, st, a, scale, g, out);
   else {
     set_error("warp_vis: channels must be 1 or 3");
     return MD2_ENOTSUP;
@@ -943,7 +498,6 @@ int launch_warp_vis(const PhotoArgs& a, const Geom& g, int C, float* out, hipStr
   return MD2_OK;
 }
 
-long photometric_blocks(int W, int H, int N) { return (long)cdiv(W, PT_W) * cdiv(H, PT_H) * N; }
 long smooth_blocks(int W, int H, int N) { return (long)cdiv(W, SM_W) * cdiv(H, SM_H) * N; }
 
 int launch_disp_sum(const float* disp, int dw, int dh, float rx, float ry, int W, int H, int N,

@@ -9,7 +9,7 @@ namespace {
 inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
 struct TailLayout {
-  size_t Rt, dRt, g_full, mean, photo[MAX_SCALES], smooth[MAX_SCALES], terms, total;
+  size_t Rt, dRt, g_full[MAX_SCALES], mean, photo[MAX_SCALES], smooth[MAX_SCALES], terms, total;
 };
 
 TailLayout layout(const LossTailCfg& c) {
@@ -22,10 +22,10 @@ TailLayout layout(const LossTailCfg& c) {
   };
   L.Rt = take(sizeof(float) * 2 * c.N * 12);
   L.dRt = take(sizeof(float) * 2 * c.N * 12);
-  L.g_full = take(sizeof(float) * (size_t)c.N * c.W * c.H);
   L.mean = take(sizeof(float) * (size_t)c.nscales * c.N * MEAN_PARTS);
   for (int s = 0; s < c.nscales; ++s) {
-    L.photo[s] = take(sizeof(float) * 25 * photometric_blocks(c.W, c.H, c.N));
+    L.g_full[s] = take(sizeof(float) * (size_t)c.N * c.W * c.H);
+    L.photo[s] = take(sizeof(float) * 25 * photometric_blocks(c.W, c.H, c.N, c.nscales));
     L.smooth[s] = take(sizeof(float) * 2 * smooth_blocks(c.W, c.H, c.N));
   }
   L.terms = take(sizeof(float) * 2 * MAX_SCALES);
@@ -54,7 +54,6 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
   char* ws = (char*)workspace;
   float* Rt = (float*)(ws + L.Rt);
   float* dRt = (float*)(ws + L.dRt);
-  float* g_full = (float*)(ws + L.g_full);
   float* mean = (float*)(ws + L.mean);
   float* tterms = terms ? terms : (float*)(ws + L.terms);
 
@@ -71,7 +70,7 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
   MD2_TRY(launch_so3_fwd(pose, 2 * c.N, c.N, c.invert_mask, Rt, st));
 
   const float up = dloss / c.divisor;
-  const long photo_blk = photometric_blocks(c.W, c.H, c.N);
+  const long photo_blk = photometric_blocks(c.W, c.H, c.N, c.nscales);
   const long smooth_blk = smooth_blocks(c.W, c.H, c.N);
   FinalizeArgs fa{};
   fa.nscales = c.nscales;
@@ -80,52 +79,56 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
   fa.terms = tterms;
   fa.divisor = c.divisor;
 
+  // all scales' warp + SSIM + L1 forward and pullback in one launch (photo.hip)
+  PhotoArgs pa{};
+  pa.nscales = c.nscales;
+  pa.x = x;
+  pa.x_sample_stride = c.x_sample_stride;
+  pa.x_frame_stride = c.x_frame_stride;
+  pa.target = c.target;
+  pa.src0 = c.src0;
+  pa.src1 = c.src1;
+  pa.Rt = Rt;
+  pa.automask = automask;
+  pa.wloss = up / ((float)c.N * c.W * c.H);
+  pa.N = c.N;
+  const size_t plane = (size_t)c.N * c.W * c.H;
   for (int s = 0; s < c.nscales; ++s) {
     MD2_CHECK_ARG(c.dw[s] >= 1 && c.dh[s] >= 1 && c.dw[s] <= c.W && c.dh[s] <= c.H, "scale dims");
-    const float rx = ratio(c.dw[s], c.W), ry = ratio(c.dh[s], c.H);
+    PhotoScale& ps = pa.sc[s];
+    ps.disp = disp[s];
+    ps.dw = c.dw[s];
+    ps.dh = c.dh[s];
+    ps.rx = ratio(c.dw[s], c.W);
+    ps.ry = ratio(c.dh[s], c.H);
+    ps.g_disp = (float*)(ws + L.g_full[s]);
+    ps.partials = (float*)(ws + L.photo[s]);
+    ps.loss_map = o.vis_loss ? o.vis_loss + s * plane : nullptr;
+    ps.sel_map = o.vis_sel ? o.vis_sel + s * plane : nullptr;
+    MD2_TRY(launch_disp_sum(disp[s], c.dw[s], c.dh[s], ps.rx, ps.ry, c.W, c.H, c.N, MEAN_PARTS,
+                            mean + (size_t)s * c.N * MEAN_PARTS, st));
+  }
+  if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[0], st));
+  MD2_TRY(launch_photometric(pa, g, c.C, st));
+  if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[1], st));
+  if (o.vis_warped) MD2_TRY(launch_warp_vis(pa, c.nscales - 1, g, c.C, o.vis_warped, st));
+
+  for (int s = 0; s < c.nscales; ++s) {
+    const PhotoScale& ps = pa.sc[s];
     float* mp = mean + (size_t)s * c.N * MEAN_PARTS;
-    float* pp = (float*)(ws + L.photo[s]);
     float* sp = (float*)(ws + L.smooth[s]);
-    MD2_TRY(launch_disp_sum(disp[s], c.dw[s], c.dh[s], rx, ry, c.W, c.H, c.N, MEAN_PARTS, mp, st));
-
-    PhotoArgs pa{};
-    pa.disp = disp[s];
-    pa.dw = c.dw[s];
-    pa.dh = c.dh[s];
-    pa.rx = rx;
-    pa.ry = ry;
-    pa.x = x;
-    pa.x_sample_stride = c.x_sample_stride;
-    pa.x_frame_stride = c.x_frame_stride;
-    pa.target = c.target;
-    pa.src0 = c.src0;
-    pa.src1 = c.src1;
-    pa.Rt = Rt;
-    pa.automask = automask;
-    pa.wloss = up / ((float)c.N * c.W * c.H);
-    pa.g_disp = g_full;
-    pa.partials = pp;
-    const size_t plane = (size_t)c.N * c.W * c.H;
-    pa.loss_map = o.vis_loss ? o.vis_loss + s * plane : nullptr;
-    pa.sel_map = o.vis_sel ? o.vis_sel + s * plane : nullptr;
-    pa.N = c.N;
-    if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[2 * s], st));
-    MD2_TRY(launch_photometric(pa, g, c.C, st));
-    if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[2 * s + 1], st));
-    if (o.vis_warped && s == c.nscales - 1) MD2_TRY(launch_warp_vis(pa, g, c.C, o.vis_warped, st));
-
     SmoothArgs sa{};
     sa.disp = disp[s];
     sa.dw = c.dw[s];
     sa.dh = c.dh[s];
-    sa.rx = rx;
-    sa.ry = ry;
+    sa.rx = ps.rx;
+    sa.ry = ps.ry;
     sa.img = x + (long)c.target * c.x_frame_stride;
     sa.img_sample_stride = c.x_sample_stride;
     sa.mean_partials = c.smooth_normalize ? mp : nullptr;
     sa.mean_parts = c.smooth_normalize ? MEAN_PARTS : 0;
     sa.ws = up * c.smooth_w[s];
-    sa.g_disp = g_full;
+    sa.g_disp = ps.g_disp;
     sa.partials = sp;
     sa.N = c.N;
     sa.W = c.W;
@@ -133,12 +136,12 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     MD2_TRY(launch_smooth(sa, c.C, st));
 
     UpAdjArgs ua{};
-    ua.g_full = g_full;
+    ua.g_full = ps.g_disp;
     ua.disp = disp[s];
     ua.dw = c.dw[s];
     ua.dh = c.dh[s];
-    ua.rx = rx;
-    ua.ry = ry;
+    ua.rx = ps.rx;
+    ua.ry = ps.ry;
     ua.mean_partials = mp;
     ua.mean_parts = MEAN_PARTS;
     ua.smooth_partials = c.smooth_normalize ? sp : nullptr;
@@ -152,7 +155,7 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     ua.H = c.H;
     if (d_disp[s]) MD2_TRY(launch_up_adjoint(ua, st));
 
-    fa.photo_partials[s] = pp;
+    fa.photo_partials[s] = ps.partials;
     fa.photo_blocks[s] = photo_blk;
     fa.smooth_partials[s] = sp;
     fa.smooth_blocks[s] = smooth_blk;
@@ -172,7 +175,7 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
 // ---------------------------------------------------------------------------------------------
 size_t warp_op_workspace_bytes(int N, int W, int H) {
   return align256(sizeof(float) * (size_t)N * W * H) +
-         align256(sizeof(float) * 25 * photometric_blocks(W, H, N));
+         align256(sizeof(float) * 25 * photometric_blocks(W, H, N, 1));
 }
 
 int warp_op_run(const WarpOpCfg& c, const float* disp, const float* Rt, const float* x,
@@ -195,11 +198,17 @@ int warp_op_run(const WarpOpCfg& c, const float* disp, const float* Rt, const fl
   g.wm1 = (float)(c.W - 1);
   g.hm1 = (float)(c.H - 1);
   PhotoArgs pa{};
-  pa.disp = disp;
-  pa.dw = c.dw;
-  pa.dh = c.dh;
-  pa.rx = ratio(c.dw, c.W);
-  pa.ry = ratio(c.dh, c.H);
+  pa.nscales = 1;
+  PhotoScale& ps = pa.sc[0];
+  ps.disp = disp;
+  ps.dw = c.dw;
+  ps.dh = c.dh;
+  ps.rx = ratio(c.dw, c.W);
+  ps.ry = ratio(c.dh, c.H);
+  ps.g_disp = g_full;
+  ps.partials = part;
+  ps.loss_map = loss_map;
+  ps.sel_map = sel_map;
   pa.x = x;
   pa.x_sample_stride = c.x_sample_stride;
   pa.x_frame_stride = c.x_frame_stride;
@@ -210,10 +219,6 @@ int warp_op_run(const WarpOpCfg& c, const float* disp, const float* Rt, const fl
   pa.automask = automask;
   pa.wloss = d_loss ? 1.f : 0.f;
   pa.gmap = d_loss;
-  pa.g_disp = g_full;
-  pa.partials = part;
-  pa.loss_map = loss_map;
-  pa.sel_map = sel_map;
   pa.N = c.N;
   MD2_TRY(launch_photometric(pa, g, c.C, st));
   if (!d_loss) return MD2_OK;
@@ -223,8 +228,8 @@ int warp_op_run(const WarpOpCfg& c, const float* disp, const float* Rt, const fl
     ua.disp = disp;
     ua.dw = c.dw;
     ua.dh = c.dh;
-    ua.rx = pa.rx;
-    ua.ry = pa.ry;
+    ua.rx = ps.rx;
+    ua.ry = ps.ry;
     ua.out = d_disp;
     ua.N = c.N;
     ua.W = c.W;
@@ -236,7 +241,7 @@ int warp_op_run(const WarpOpCfg& c, const float* disp, const float* Rt, const fl
     fa.nscales = 1;
     fa.N = c.N;
     fa.photo_partials[0] = part;
-    fa.photo_blocks[0] = photometric_blocks(c.W, c.H, c.N);
+    fa.photo_blocks[0] = photometric_blocks(c.W, c.H, c.N, 1);
     MD2_TRY(launch_pose_grad_reduce(fa, d_Rt, st));
   }
   return MD2_OK;

@@ -32,7 +32,7 @@ struct LossTailOut {
   float* vis_loss;
   signed char* vis_sel;
   float* vis_warped;                    // [2][N][C][H][W] warped sources at the last scale or nullptr
-  hipEvent_t* photo_events = nullptr;   // optional [2*nscales] around each photometric launch
+  hipEvent_t* photo_events = nullptr;   // optional [2]: around the (all-scale) photometric launch
 };
 
 // disp[s]: [N][dh][dw] sigmoid outputs; pose: [2N][6] (rvec, tvec) per (source, sample);

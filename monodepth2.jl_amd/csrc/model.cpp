@@ -735,7 +735,7 @@ class Model {
     o.d_pose = d_pose;
     hipEvent_t pev[2 * MAX_SCALES] = {};
     if (prof) {
-      for (int k = 0; k < 2 * tail.nscales; ++k) pev[k] = ev();
+      for (int k = 0; k < 2; ++k) pev[k] = ev();
       o.photo_events = pev;
     }
     if (cfg.automask && !automask) {
@@ -747,9 +747,10 @@ class Model {
     }
     MD2_TRY(loss_tail_run(tail, disps, pose, x, cfg.automask ? automask : nullptr, 1.f, o, tail_ws, st));
     if (prof) {
-      // algorithmic bytes per pixel and scale: disparity 4 + target 4C + two sources 8C + d_disp 4
-      const double bytes = (double)N * cfg.H * cfg.W * (8.0 + 12.0 * cfg.arch.in_ch);
-      for (int k = 0; k < tail.nscales; ++k) recs.push_back({pev[2 * k], pev[2 * k + 1], PROF_PHOTO, bytes});
+      // one launch for all scales; algorithmic bytes per full-res pixel and scale:
+      // disparity 4 + target 4C + two sources 8C + d_disp 4
+      const double bytes = (double)tail.nscales * N * cfg.H * cfg.W * (8.0 + 12.0 * cfg.arch.in_ch);
+      recs.push_back({pev[0], pev[1], PROF_PHOTO, bytes});
     }
     return MD2_OK;
   }

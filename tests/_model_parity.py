@@ -81,6 +81,32 @@ def gpu_decisions(model, N, arch=18, L=3):
     return d
 
 
+def oracle_at_gpu_outputs(g, N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7):
+    """The fp64 oracle's gradient with the loss tail evaluated AT THE GPU's forward outputs
+    (disparities, poses) and back-propagated through the oracle's own networks (value substituted,
+    graph kept: d_o + (d_gpu - d_o).detach()).  Against the plain oracle this isolates how much
+    of a gradient difference the ~1e-6 forward discrepancy alone explains; against the GPU it
+    measures the backward's own accuracy."""
+    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
+    K, invK = D.intrinsics(W, H)
+    spec = O.param_spec(arch, C, (2, 3, 4, 5))
+    f = g["flat"].double().clone().requires_grad_(True)
+    P = O.unflatten(f, spec)
+    with O.forced_decisions(g["decisions"]):
+        d_o, p_o = O.model_forward(P, x, arch=arch)
+    d_s = [d + (dg.double().view_as(d) - d).detach() for d, dg in zip(d_o, g["disps"])]
+    pg = g["pose"].double()
+    p_s = []
+    for k, (r, t) in enumerate(p_o):
+        q = pg[k * N:(k + 1) * N]
+        p_s.append((r + (q[:, :3] - r).detach(), t + (q[:, 3:] - t).detach()))
+    cache_o = O.TrainCache(K=K, invK=invK)
+    par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
+    forced = [s.unsqueeze(1).long() for s in g["sel"]]
+    O.loss_from_outputs(d_s, p_s, x, None, cache_o, par_o, forced_sel=forced).backward()
+    return f.grad.double()
+
+
 def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=None, sel=None,
                       decisions=None):
     """Per-tensor gradient error of the SAME oracle run in fp32 vs fp64 (the fp32 noise floor),

@@ -1,10 +1,24 @@
-set -e
+#!/bin/bash
+# Counters of the loss-tail kernels (photometric_kernel et al.) at the bench shape, one pass per
+# counter group (tools/photo_one.py N iters).  Usage: tools/pmc_photo.sh TAG [N...]
+# Output: gpurun_out/pmc_photo_<TAG>/<N>/{trace,a,b,c,fetch,write}; summarise with
+#   python tools/pmc_report.py gpurun_out/pmc_photo_<TAG>/<N>
+set -euo pipefail
+TAG=${1:-cur}
+shift || true
+NS=${*:-12 96}
 R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out/pp
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 120 python3 $R/tools/photo_one.py 12 12 > $R/gpurun_out/pp/plain.txt 2>&1
-rocprofv3 -L > /tmp/counters.txt 2>&1 || true
-grep -o "SQ_[A-Z_0-9]*" /tmp/counters.txt | sort -u > $R/gpurun_out/pp/sq_counters.txt || true
-timeout -k 10 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS -d $R/gpurun_out/pp/p1 -o run --output-format csv -- python3 $R/tools/photo_one.py 12 4 > /dev/null 2>&1
-timeout -k 10 200 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM GRBM_GUI_ACTIVE -d $R/gpurun_out/pp/p2 -o run --output-format csv -- python3 $R/tools/photo_one.py 12 4 > /dev/null 2>&1
-echo done
+for N in $NS; do
+  OUT=$R/gpurun_out/pmc_photo_$TAG/$N
+  mkdir -p "$OUT"
+  P="$R/tools/photo_one.py $N 6"
+  timeout -k 10 120 python3 $P > "$OUT/plain.txt" 2>&1
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $P > /dev/null
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU -d "$OUT/a" -o run --output-format csv -- python3 $P > /dev/null
+  timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE -d "$OUT/b" -o run --output-format csv -- python3 $P > /dev/null
+  timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_FLAT SQ_INST_LEVEL_LDS SQ_WAIT_INST_ANY -d "$OUT/c" -o run --output-format csv -- python3 $P > /dev/null
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 $P > /dev/null
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 $P > /dev/null
+done
+echo "pmc done"
