@@ -312,6 +312,11 @@ int md2_model_features(md2_model* m, const float** feat, int* c, int* h, int* w)
 #define MD2_PROF_NCAT 3
 int md2_model_set_profiling(md2_model* m, int on);
 int md2_model_profile_read(md2_model* m, double* out, int ncat);
+/* the same events one record at a time (per-layer table): ms, work, category and a tag ("fwd
+ * 3x3/1 64->64 32x104 n36" for a conv: pass, kernel/stride[r = reflect pad], channels, input
+ * size, images); up to `max` records, *count set; clears like md2_model_profile_read. */
+int md2_model_profile_records(md2_model* m, int max, double* ms, double* work, int* cat, char* tags,
+                              int tag_len, int* count);
 /* Diagnostics (parity tests): named internal buffers of the last forward / backward, by index
  * 0..count-1 (MD2_EINVAL past the end): encoder activations ("stem.y", "stem.out",
  * "maxpool.out", "maxpool.arg" = window index kh*3+kw as uint8, "layer<s>.<b>.conv<k>.y",

@@ -381,6 +381,12 @@ int md2_model_profile_read(md2_model* m, double* out, int ncat) {
   return model_profile_read(m->impl, out, ncat);
 }
 
+int md2_model_profile_records(md2_model* m, int max, double* ms, double* work, int* cat, char* tags,
+                              int tag_len, int* count) {
+  MD2_CHECK_ARG(m, "model");
+  return model_profile_records(m->impl, max, ms, work, cat, tags, tag_len, count);
+}
+
 int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose) {
   MD2_CHECK_ARG(m, "model");
   return model_outputs(m->impl, disp, w, h, pose);

@@ -517,6 +517,7 @@ class Model {
     hipEvent_t a, b;
     int cat;
     double work;
+    char tag[64];   // pass + shape of a conv record (per-layer table), "" otherwise
   };
   bool prof = false;
   std::vector<ProfRec> recs;
@@ -536,11 +537,16 @@ class Model {
     (void)hipEventRecord(e, st);
     return e;
   }
-  void prof_end(hipEvent_t a, int cat, double work, hipStream_t st) {
+  void prof_end(hipEvent_t a, int cat, double work, hipStream_t st, const char* pass = nullptr,
+                const ConvShape* s = nullptr) {
     if (!prof) return;
     hipEvent_t b = ev();
     (void)hipEventRecord(b, st);
-    recs.push_back({a, b, cat, work});
+    ProfRec r{a, b, cat, work, {0}};
+    if (pass && s)
+      snprintf(r.tag, sizeof(r.tag), "%s %dx%d/%d%s %d->%d %dx%d n%d", pass, s->KH, s->KW, s->stride,
+               s->reflect ? "r" : "", s->Cin, s->Cout, s->H, s->W, s->N);
+    recs.push_back(r);
   }
   static double conv_flops(const ConvShape& s) {
     return 2.0 * s.N * (double)s.Ho * s.Wo * s.Cout * s.Cin * s.KH * s.KW;
@@ -558,7 +564,7 @@ class Model {
     o.accumulate = accumulate;
     hipEvent_t e = prof_begin(st);
     MD2_TRY(conv_fwd(s, in, c.wpf, o, cws, st));
-    prof_end(e, c.cat, conv_flops(s), st);
+    prof_end(e, c.cat, conv_flops(s), st, "fwd", &s);
     return MD2_OK;
   }
   static TensorIn tin(const float* p, int C, long HW) {
@@ -750,8 +756,32 @@ class Model {
       // one launch for all scales; algorithmic bytes per full-res pixel and scale:
       // disparity 4 + target 4C + two sources 8C + d_disp 4
       const double bytes = (double)tail.nscales * N * cfg.H * cfg.W * (8.0 + 12.0 * cfg.arch.in_ch);
-      recs.push_back({pev[0], pev[1], PROF_PHOTO, bytes});
+      recs.push_back({pev[0], pev[1], PROF_PHOTO, bytes, "photometric (all scales)"});
     }
+    return MD2_OK;
+  }
+
+  // per-record view of the same events (per-layer table); clears like profile_read
+  int profile_records(int max, double* ms, double* work, int* cat, char* tags, int tag_len,
+                      int* count) {
+    int k = 0;
+    for (auto& r : recs) {
+      if (k >= max) break;
+      MD2_HIP(hipEventSynchronize(r.b));
+      float t = 0.f;
+      MD2_HIP(hipEventElapsedTime(&t, r.a, r.b));
+      ms[k] = t;
+      work[k] = r.work;
+      cat[k] = r.cat;
+      if (tags && tag_len > 0) {
+        strncpy(tags + (long)k * tag_len, r.tag, tag_len - 1);
+        tags[(long)k * tag_len + tag_len - 1] = 0;
+      }
+      ++k;
+    }
+    *count = k;
+    recs.clear();
+    evi = 0;
     return MD2_OK;
   }
 
@@ -780,7 +810,7 @@ class Model {
     MD2_TRY(conv_wgrad(s, in, dy, grads + c.p.w, Gd(c.p.b), 0, cws, st, c.p.b >= 0 ? bp_pending : nullptr,
                        bp_parts));
     bp_pending = nullptr;
-    prof_end(e, c.cat, conv_flops(s), st);
+    prof_end(e, c.cat, conv_flops(s), st, "wgrad", &s);
     return MD2_OK;
   }
   // filter and data gradient of one conv from the same dY.  (Running the filter gradient on a
@@ -804,7 +834,7 @@ class Model {
     o.accumulate = acc;
     hipEvent_t e = prof_begin(st);
     MD2_TRY(conv_dgrad(s, dy, c.wpd, o, cws, st));
-    prof_end(e, c.cat, conv_flops(s), st);
+    prof_end(e, c.cat, conv_flops(s), st, "dgrad", &s);
     return MD2_OK;
   }
   // activation pullback fused with the bias-gradient partials of the conv that produced `out`
@@ -1119,6 +1149,12 @@ int model_set_profiling(Model* m, int on) {
   m->recs.clear();
   m->evi = 0;
   return MD2_OK;
+}
+
+int model_profile_records(Model* m, int max, double* ms, double* work, int* cat, char* tags,
+                          int tag_len, int* count) {
+  MD2_CHECK_ARG(m && ms && work && cat && count && max >= 0, "profile_records args");
+  return m->profile_records(max, ms, work, cat, tags, tag_len, count);
 }
 
 int model_profile_read(Model* m, double* out, int ncat) {

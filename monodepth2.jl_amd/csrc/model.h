@@ -46,6 +46,8 @@ class Model;
 int model_set_profiling(Model* m, int on);
 // out[cat*3 + {0,1,2}] = {total ms, total algorithmic work (FLOP or bytes), launches}
 int model_profile_read(Model* m, double* out, int ncat);
+int model_profile_records(Model* m, int max, double* ms, double* work, int* cat, char* tags,
+                          int tag_len, int* count);
 int model_create(const ModelCfg& cfg, float* params, float* grads, Model** out);
 void model_destroy(Model* m);
 

@@ -136,6 +136,8 @@ _SIGS = {
     "md2_warp_photometric_bwd": (C.c_int, [C.POINTER(WarpCfg), P, P, P, P, P, P, P, P, P]),
     "md2_model_set_profiling": (C.c_int, [P, C.c_int]),
     "md2_model_profile_read": (C.c_int, [P, C.POINTER(C.c_double), C.c_int]),
+    "md2_model_profile_records": (C.c_int, [P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                            C.POINTER(C.c_int), C.c_char_p, C.c_int, C.POINTER(C.c_int)]),
 }
 
 

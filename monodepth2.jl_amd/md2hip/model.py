@@ -179,6 +179,21 @@ class _Executor:
         check(lib().md2_model_profile_read(self.handle, buf, n), "md2_model_profile_read")
         return {c: (buf[3 * i], buf[3 * i + 1], int(buf[3 * i + 2])) for i, c in enumerate(self.PROF_CATS)}
 
+    def profile_records(self, max_records=4096):
+        """[(tag, category, ms, work)] per profiled launch (per-layer table), then clears."""
+        ms = (C.c_double * max_records)()
+        work = (C.c_double * max_records)()
+        cat = (C.c_int * max_records)()
+        tag_len = 64
+        tags = C.create_string_buffer(max_records * tag_len)
+        count = C.c_int(0)
+        check(lib().md2_model_profile_records(self.handle, max_records, ms, work, cat, tags, tag_len,
+                                              C.byref(count)), "md2_model_profile_records")
+        raw = tags.raw
+        return [(raw[i * tag_len:(i + 1) * tag_len].split(b"\0", 1)[0].decode(),
+                 self.PROF_CATS[cat[i]] if cat[i] < len(self.PROF_CATS) else str(cat[i]), ms[i], work[i])
+                for i in range(count.value)]
+
     def forward_loss(self, x, auto_loss=None, loss=None, terms=None):
         import torch
         loss = loss if loss is not None else torch.empty(1, dtype=torch.float32, device=x.device)
