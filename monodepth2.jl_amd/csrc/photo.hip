@@ -453,10 +453,9 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
     __builtin_amdgcn_sched_barrier(0);
     float cf[2][C][3];
     const int sel = p2_head(Sc, R - 1, am, gp, cf);
-    __builtin_amdgcn_sched_barrier(0);
+    // the next row's loads may interleave with the SSIM arithmetic (measured: 147 -> 136 us)
     issue_gathers(R + 1);                          // rows past the tile are harmless (clamped)
     issue_disp(R + 2);
-    __builtin_amdgcn_sched_barrier(0);
     p2_tail_p3(Sc, sel, cf, R - 2, k >= 4 && k < KT, selc, gpc);
     selc = sel;
     gpc = gp;

@@ -12,7 +12,7 @@ for v in base ${VARIANTS:-}; do
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
     n = r["Name"]
-    if any(k in n for k in ("photometric", "smooth_kernel", "up_adjoint", "disp_sum")):
+    if any(k in n for k in ("photo", "smooth_kernel", "up_adjoint", "disp_sum")):
         print(f"{n[:60]:60s} calls={r['Calls']} avg_us={float(r['AverageNs'])/1000:.1f}")
 PY
 done
