@@ -127,6 +127,13 @@ int md2_so3_compose_bwd(const float* pose, int n, int invert_mask, const float* 
  * ---------------------------------------------------------------------------------------- */
 int md2_automasking_loss(const float* x, int n, int c, int h, int w, int target, int src0,
                          int src1, float* out, void* stream);
+/* find_static(dataset, alpha) (src/dtk.jl:51-69), the per-sample part: scores[i] =
+ * mean(automasking_loss(ssim, x_i, x_i[target]; source_ids)) for the n triplets of x
+ * [n][3][c][h][w]; the dataset filter keeps samples with scores[i] > alpha (md2hip.find_static).
+ * workspace: md2_static_scores_workspace_size(n, h, w) bytes of device memory. */
+size_t md2_static_scores_workspace_size(int n, int h, int w);
+int md2_static_scores(const float* x, int n, int c, int h, int w, int target, int src0, int src1,
+                      float* scores, void* workspace, void* stream);
 int md2_ssim_fwd(const float* x, const float* y, int n, int c, int h, int w, float* out,
                  void* stream);
 int md2_ssim_bwd(const float* x, const float* y, const float* dout, int n, int c, int h, int w,

@@ -404,6 +404,28 @@ function ChainRulesCore.rrule(::typeof(so3_compose), pose::ROCArray{Float32,2}, 
     return Rt, so3_compose_pullback
 end
 
+# find_static(dataset, α) -- src/dtk.jl:51-69: per-triplet mean identity-reprojection loss of a
+# batch x (W,H,C,3,n) on the GPU; the dataset keeps the files whose score exceeds α
+function static_scores(x::ROCArray{Float32,5}; target_id=2, source_ids=(1, 3))
+    W, H, C, L, n = size(x); scores = ROCVector{Float32}(undef, n)
+    ws = ROCVector{UInt8}(undef, ccall((:md2_static_scores_workspace_size, lib), Csize_t, (Cint, Cint, Cint), n, H, W))
+    check(ccall((:md2_static_scores, lib), Cint,
+                (Ptr{Float32}, Cint, Cint, Cint, Cint, Cint, Cint, Cint, Ptr{Float32}, Ptr{UInt8}, Ptr{Cvoid}),
+                x, n, C, H, W, target_id - 1, source_ids[1] - 1, source_ids[2] - 1, scores, ws, stream_ptr()))
+    return Array(scores)
+end
+
+function find_static(dataset, α; batch=16)
+    keep = String[]
+    for b0 in 1:batch:length(dataset)
+        idx = b0:min(length(dataset), b0 + batch - 1)
+        x = ROCArray(cat([dataset[i] for i in idx]...; dims=5))
+        s = static_scores(x; target_id=dataset.target_id, source_ids=dataset.source_ids)
+        append!(keep, dataset.files[idx][s .> α])
+    end
+    return keep
+end
+
 # ------------------------------------------------------------------------------------------------
 # Data parallel: one Julia process per GPU over the library's own RCCL communicator (SURVEY 8e;
 # the reference's loop is scripts/script.jl:84-86).  Rank 0 writes the unique id to `idfile`.

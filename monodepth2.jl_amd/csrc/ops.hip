@@ -409,6 +409,18 @@ __global__ __launch_bounds__(256) void grid_sample_bwd_kernel(const float* __res
 
 }  // namespace
 
+// per-sample mean of an [n][hw] map, one block per sample, fixed summation order (deterministic)
+__global__ __launch_bounds__(256) void sample_mean_kernel(const float* __restrict__ m, long hw,
+                                                          float* __restrict__ out) {
+  __shared__ float red[4];
+  const float* p = m + (long)blockIdx.x * hw;
+  float s = 0.f;
+  for (long i = threadIdx.x; i < hw; i += 256) s += p[i];
+  float v[1] = {s};
+  block_sum256<1>(v, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = v[0] / (float)hw;
+}
+
 int launch_automask(const float* x, long x_sample_stride, long x_frame_stride, int target,
                     int src0, int src1, int N, int C, int H, int W, float* out, hipStream_t st) {
   const dim3 grid(cdiv(W, OT_W), cdiv(H, OT_H), N);
@@ -448,6 +460,26 @@ int md2_automasking_loss(const float* x, int n, int c, int h, int w, int target,
                 "frame ids (0-based, < 3)");
   const long fs = (long)c * h * w;
   return launch_automask(x, 3 * fs, fs, target, src0, src1, n, c, h, w, out, (hipStream_t)stream);
+}
+
+size_t md2_static_scores_workspace_size(int n, int h, int w) {
+  return a256(sizeof(float) * (size_t)n * h * w);
+}
+
+// find_static (src/dtk.jl:51-69): score[i] = mean(automasking_loss(ssim, x_i, x_i[target];
+// source_ids)); the caller keeps the samples whose score exceeds alpha
+int md2_static_scores(const float* x, int n, int c, int h, int w, int target, int src0, int src1,
+                      float* scores, void* workspace, void* stream) {
+  MD2_CHECK_ARG(x && scores && workspace && n > 0 && w >= 2 && h >= 2, "static_scores args");
+  MD2_CHECK_ARG(target >= 0 && target < 3 && src0 >= 0 && src0 < 3 && src1 >= 0 && src1 < 3,
+                "frame ids (0-based, < 3)");
+  const long fs = (long)c * h * w;
+  float* map = (float*)workspace;
+  MD2_TRY(launch_automask(x, 3 * fs, fs, target, src0, src1, n, c, h, w, map, (hipStream_t)stream));
+  hipLaunchKernelGGL(sample_mean_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, map,
+                     (long)h * w, scores);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
 }
 
 int md2_ssim_fwd(const float* x, const float* y, int n, int c, int h, int w, float* out,

@@ -10,12 +10,12 @@ from .model import (ADAM, DepthDecoder, Model, Pose, PoseDecoder, ResidualNetwor
                     eval_disparity, gradient, param_table, train_loss, train_step)
 from .slow_depth import SlowDepth, adam_update, slow_depth  # noqa: F401
 from .checkpoint import load_checkpoint, save_checkpoint  # noqa: F401
-from .data import DataLoader, DChain, Depth10k, FlipX, KittyDataset  # noqa: F401
+from .data import DataLoader, DChain, Depth10k, FlipX, KittyDataset, find_static  # noqa: F401
 from .mpi import MPIDepthDecoder, mpi_forward  # noqa: F401
 
 __all__ = ["Params", "TrainCache", "depth10k_intrinsics", "loss_tail", "pack_poses", "lib", "MD2Error",
            "ADAM", "DepthDecoder", "Model", "Pose", "PoseDecoder", "ResidualNetwork", "ResNet",
            "eval_disparity", "gradient", "param_table", "train_loss", "train_step",
            "SlowDepth", "adam_update", "slow_depth", "load_checkpoint", "save_checkpoint",
-           "DataLoader", "DChain", "Depth10k", "FlipX", "KittyDataset",
+           "DataLoader", "DChain", "Depth10k", "FlipX", "KittyDataset", "find_static",
            "MPIDepthDecoder", "mpi_forward"]

@@ -118,6 +118,8 @@ _SIGS = {
                                          C.c_int, P, P]),
     "md2_concat_channels": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_longlong, P, P]),
     "md2_automasking_loss": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "md2_static_scores_workspace_size": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    "md2_static_scores": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
     "md2_ssim_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "md2_ssim_bwd": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
     "md2_backproject_fwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, P, P, P]),

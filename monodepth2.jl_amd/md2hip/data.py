@@ -278,3 +278,21 @@ class DataLoader:
                 except queue.Empty:
                     pass
             t.join()
+
+
+def find_static(dataset, alpha: float, batch: int = 16, device=None, seed: int = 0) -> List[str]:
+    """``find_static(dataset, α)`` (src/dtk.jl:51-69): the files of the samples whose mean
+    identity-reprojection loss (``automasking_loss`` of the raw frames against the target) exceeds
+    ``alpha`` -- the non-static triplets, in dataset order.  Scores on the GPU in batches
+    (``md2_static_scores``); no CPU fallback."""
+    import torch
+    from .primitives import static_scores
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    src = tuple(dataset.source_ids)
+    keep: List[str] = []
+    for b0 in range(0, len(dataset), batch):
+        idx = list(range(b0, min(len(dataset), b0 + batch)))
+        x = torch.from_numpy(np.stack([dataset.getobs(i, seed) for i in idx])).to(dev).contiguous()
+        scores = static_scores(x, dataset.target_id, src).cpu().tolist()
+        keep.extend(dataset.files[i] for i, s in zip(idx, scores) if s > alpha)
+    return keep

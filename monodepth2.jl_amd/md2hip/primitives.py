@@ -35,6 +35,22 @@ def _ws(nbytes, dev):
 
 
 # ------------------------------------------------------------------------------------------------
+def static_scores(x, target_id: int = 2, source_ids: Sequence[int] = (1, 3)):
+    """Per-sample ``mean(automasking_loss(ssim, x_i, x_i[target]; source_ids))`` -- the score
+    ``find_static`` (src/dtk.jl:51-69) thresholds.  x [N, 3, C, H, W] -> [N]."""
+    import torch
+    _f32(x)
+    N, L, Cc, H, W = x.shape
+    if L != 3 or len(source_ids) != 2:
+        raise ValueError("x must hold 3 frames and source_ids two of them")
+    out = torch.empty(N, dtype=torch.float32, device=x.device)
+    ws = _ws(lib().md2_static_scores_workspace_size(N, H, W), x.device)
+    check(lib().md2_static_scores(ptr(x), N, Cc, H, W, target_id - 1, source_ids[0] - 1,
+                                  source_ids[1] - 1, ptr(out), ptr(ws), stream_of(x.device)),
+          "md2_static_scores")
+    return out
+
+
 def automasking_loss(x, target_id: int = 2, source_ids: Sequence[int] = (1, 3)):
     """``automasking_loss(ssim, x, target; source_ids)`` (src/training.jl:9-11): x [N, 3, C, H, W]
     -> [N, 1, H, W] identity-reprojection loss (min over the raw sources).  Data only."""

@@ -223,6 +223,22 @@ def automasking_loss(inputs: torch.Tensor, target: torch.Tensor, source_ids: Seq
     return _first_argmin([photometric_loss(inputs[:, i - 1], target) for i in source_ids])
 
 
+def static_scores(inputs: torch.Tensor, target_id: int = 2, source_ids: Sequence[int] = (1, 3)):
+    """The per-sample score of ``find_static`` -- src/dtk.jl:51-69: mean(automasking_loss(ssim,
+    x, x[target]; source_ids)) of each triplet.  inputs [N,L,C,H,W] -> [N]."""
+    am = automasking_loss(inputs, inputs[:, target_id - 1], source_ids)
+    return am.flatten(1).mean(1)
+
+
+def find_static(samples, files, alpha, target_id=2, source_ids=(1, 3)):
+    """``find_static(dataset, α)`` -- src/dtk.jl:51-69: the files whose score exceeds alpha."""
+    keep = []
+    for x, f in zip(samples, files):
+        if static_scores(x.unsqueeze(0), target_id, source_ids)[0].item() > alpha:
+            keep.append(f)
+    return keep
+
+
 def prediction_loss(predictions: Sequence[torch.Tensor], target: torch.Tensor):
     """``prediction_loss`` -- src/training.jl:13-15."""
     return _first_argmin([photometric_loss(p, target) for p in predictions])
