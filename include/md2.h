@@ -227,6 +227,40 @@ int md2_concat_channels(const float* a, int ca, const float* b, int cb, int n, l
                         float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * MINE plane rendering of the MPI mode (src/render.jl:21-114), forward (the reference defines
+ * no pullback).  Arrays are the Julia arrays' bytes (column-major dims listed first):
+ *   rgb (W,H,3,N,B)   sigma (W,H,1,N,B)   xyz (3,W,H,N,B)   disparity/depth (N,B)
+ *   pose [B][6] = (rvec, tvec) of Pose(rvec (3,B), tvec (3,B))   K, invK 3x3 row-major (host)
+ * The reference's semantics are reproduced as written (valid mask = chained comparison
+ * u < W*u >= 0, grid normalised (u + 0.5)/(W/2) with no -1, last plane distance 1e3,
+ * transmittance over T + 1e-6); see DESIGN.md "MINE rendering".
+ * md2_mine_src_xyz   get_src_xyz_from_plane_disparity(create_meshgrid(H,W), disparity, invK)
+ *                    (render.jl:21-30) -> xyz (3,W,H,N,B)
+ * md2_mine_tgt_xyz   get_tgt_xyz_from_plane_disparity(xyz_src, pose) (render.jl:51-64)
+ * md2_mine_sample    sample(src, depth_src, pose, K, K_inv) (render.jl:66-94): src (W,H,c,N*B),
+ *                    depth (N,B) -> out (W,H,c,N*B), valid (W*H, N*B) as 0/1 floats
+ * md2_plane_volume_rendering  plane_volume_rendering(rgb, sigma, xyz) (render.jl:32-49) ->
+ *                    rgb_out (W,H,3,B), transparency_acc (W,H,1,N,B), weights (W,H,1,N,B)
+ * md2_render_tgt_rgb_depth  render_tgt_rgb_depth(rgb, sigma, disparity, xyz_tgt, pose, invK, K)
+ *                    (render.jl:96-114), one fused kernel, N <= 512 -> rgb (W,H,3,B),
+ *                    depth (W,H,1,N,B), mask (W,H,1,1,B) (plane counts of the valid mask)
+ * ---------------------------------------------------------------------------------------- */
+int md2_mine_src_xyz(const float* disparity, int n_planes, int batch, int h, int w,
+                     const float* invK, float* xyz, void* stream);
+int md2_mine_tgt_xyz(const float* xyz_src, const float* pose, int n_planes, int batch, int h, int w,
+                     float* xyz_tgt, void* stream);
+int md2_mine_sample(const float* src, int c, const float* depth, const float* pose, int n_planes,
+                    int batch, int h, int w, const float* K, const float* invK, float* out,
+                    float* valid, void* stream);
+int md2_plane_volume_rendering(const float* rgb, const float* sigma, const float* xyz, int n_planes,
+                               int batch, int h, int w, float* rgb_out, float* transparency_acc,
+                               float* weights, void* stream);
+int md2_render_tgt_rgb_depth(const float* rgb, const float* sigma, const float* disparity,
+                             const float* xyz_tgt, const float* pose, const float* invK,
+                             const float* K, int n_planes, int batch, int h, int w, float* rgb_out,
+                             float* depth, float* mask, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Model: Model(ResidualNetwork(arch), DepthDecoder(embedding_levels=0), PoseDecoder) in mono
  * mode (src/model.jl:24-70), train_loss (src/training.jl:21-78), its pullback, Flux ADAM.
  * Parameters / gradients are CALLER-owned flat fp32 device vectors; their order is the table
@@ -239,12 +273,14 @@ typedef struct md2_model_cfg {
   int batch;                            /* samples per step (triplets)                       */
   int width, height;                    /* Params.target_size (multiples of 32)              */
   int n_levels;                         /* length(scale_levels)                              */
-  int scale_levels[MD2_MAX_SCALES];     /* DepthDecoder scale_levels, increasing, last == 5  */
+  int scale_levels[MD2_MAX_SCALES];     /* DepthDecoder scale_levels in 1:5, strictly increasing
+                                           (repeated / decreasing: MD2_ENOTSUP)               */
   float K[9], invK[9];                  /* TrainCache.K / invK, row-major                    */
   float min_depth, max_depth, disparity_smoothness;   /* Params                              */
   float scales[MD2_MAX_SCALES];         /* TrainCache.scales                                 */
   int automasking;                      /* Params.automasking                                */
-  int target, src0, src1;               /* 0-based frame ids (only 1, 0, 2 supported)        */
+  int target, src0, src1;               /* 0-based frame ids in 0:2 (TrainCache target_id /
+                                           source_ids minus 1)                                */
 } md2_model_cfg;
 
 typedef struct md2_model md2_model;

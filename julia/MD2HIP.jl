@@ -427,6 +427,69 @@ function find_static(dataset, α; batch=16)
 end
 
 # ------------------------------------------------------------------------------------------------
+# MINE plane rendering of the MPI mode (src/render.jl:21-114), forward only as upstream.  Same
+# names and argument order as the reference; `pose` is a Pose(rvec (3,B), tvec (3,B)) and goes to
+# the library as (6,B) = [B][6]; K / invK are host 3x3 matrices.
+# ------------------------------------------------------------------------------------------------
+pose6(pose) = ROCArray{Float32}(vcat(reshape(pose.rvec, 3, :), reshape(pose.tvec, 3, :)))
+
+function get_src_xyz_from_plane_disparity(meshgrid_src_homo, mpi_disparity_src::ROCArray{Float32,2}, K_src_inv)
+    _, W, H = size(meshgrid_src_homo)                  # create_meshgrid(H, W): the kernel's grid
+    N, B = size(mpi_disparity_src); xyz = ROCArray{Float32}(undef, 3, W, H, N, B)
+    iK = collect(rowmajor(K_src_inv))
+    check(ccall((:md2_mine_src_xyz, lib), Cint,
+                (Ptr{Float32}, Cint, Cint, Cint, Cint, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                mpi_disparity_src, N, B, H, W, iK, xyz, stream_ptr()))
+    return xyz
+end
+
+function get_tgt_xyz_from_plane_disparity(xyz_src::ROCArray{Float32,5}, pose)
+    _, W, H, N, B = size(xyz_src); out = similar(xyz_src)
+    check(ccall((:md2_mine_tgt_xyz, lib), Cint,
+                (Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Ptr{Float32}, Ptr{Cvoid}),
+                xyz_src, pose6(pose), N, B, H, W, out, stream_ptr()))
+    return out
+end
+
+# sample(src (W,H,C,N*B), depth_src (N,B), pose, K, K_inv) -> (tgt, valid_mask (W*H, N*B))
+function sample(src::ROCArray{Float32,4}, depth_src::ROCArray{Float32,2}, pose, K, K_inv)
+    W, H, C, NB = size(src); N, B = size(depth_src)
+    tgt = similar(src); valid = ROCArray{Float32}(undef, W * H, NB)
+    k = collect(rowmajor(K)); ik = collect(rowmajor(K_inv))
+    check(ccall((:md2_mine_sample, lib), Cint,
+                (Ptr{Float32}, Cint, Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Ptr{Float32},
+                 Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                src, C, depth_src, pose6(pose), N, B, H, W, k, ik, tgt, valid, stream_ptr()))
+    return tgt, valid .> 0
+end
+
+function plane_volume_rendering(rgb::ROCArray{Float32,5}, sigma::ROCArray{Float32,5}, xyz::ROCArray{Float32,5})
+    W, H, _, N, B = size(rgb)
+    rgb_out = ROCArray{Float32}(undef, W, H, 3, B)
+    acc = ROCArray{Float32}(undef, W, H, 1, N, B); weights = similar(acc)
+    check(ccall((:md2_plane_volume_rendering, lib), Cint,
+                (Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Ptr{Float32},
+                 Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                rgb, sigma, xyz, N, B, H, W, rgb_out, acc, weights, stream_ptr()))
+    return rgb_out, acc, weights
+end
+
+# one fused kernel: homography warp of rgb/sigma/xyz per plane + volume rendering + valid count
+function render_tgt_rgb_depth(rgb::ROCArray{Float32,5}, sigma::ROCArray{Float32,5},
+                              disparity_src::ROCArray{Float32,2}, xyz_tgt::ROCArray{Float32,5}, pose, K_inv, K)
+    W, H, _, N, B = size(rgb)
+    rgb_out = ROCArray{Float32}(undef, W, H, 3, B)
+    depth = ROCArray{Float32}(undef, W, H, 1, N, B); mask = ROCArray{Float32}(undef, W, H, 1, 1, B)
+    ik = collect(rowmajor(K_inv)); k = collect(rowmajor(K))
+    check(ccall((:md2_render_tgt_rgb_depth, lib), Cint,
+                (Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32},
+                 Ptr{Float32}, Cint, Cint, Cint, Cint, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                rgb, sigma, disparity_src, xyz_tgt, pose6(pose), ik, k, N, B, H, W, rgb_out, depth, mask,
+                stream_ptr()))
+    return rgb_out, depth, mask
+end
+
+# ------------------------------------------------------------------------------------------------
 # Data parallel: one Julia process per GPU over the library's own RCCL communicator (SURVEY 8e;
 # the reference's loop is scripts/script.jl:84-86).  Rank 0 writes the unique id to `idfile`.
 # ------------------------------------------------------------------------------------------------

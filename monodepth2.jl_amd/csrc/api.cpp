@@ -7,6 +7,7 @@
 
 #include "conv.h"
 #include "loss_tail.h"
+#include "mine.h"
 #include "model.h"
 #include "nn.h"
 
@@ -256,6 +257,50 @@ int md2_concat_channels(const float* a, int ca, const float* b, int cb, int n, l
   MD2_CHECK_ARG(a && b && out && ca > 0 && cb > 0 && n > 0 && hw > 0, "concat_channels args");
   return concat_channels(a, ca, b, cb, n, (long)hw, out, (hipStream_t)stream);
 }
+// ---- MINE rendering (src/render.jl:21-114) -------------------------------------------------
+static md2::Mat3 mat3(const float* m) {
+  md2::Mat3 r;
+  std::memcpy(r.m, m, sizeof(r.m));
+  return r;
+}
+int md2_mine_src_xyz(const float* disparity, int n_planes, int batch, int h, int w,
+                     const float* invK, float* xyz, void* stream) {
+  MD2_CHECK_ARG(disparity && invK && xyz && n_planes > 0 && batch > 0 && h > 0 && w > 0,
+                "mine_src_xyz args");
+  return mine_src_xyz(disparity, n_planes, batch, h, w, mat3(invK), xyz, (hipStream_t)stream);
+}
+int md2_mine_tgt_xyz(const float* xyz_src, const float* pose, int n_planes, int batch, int h, int w,
+                     float* xyz_tgt, void* stream) {
+  MD2_CHECK_ARG(xyz_src && pose && xyz_tgt && n_planes > 0 && batch > 0 && h > 0 && w > 0,
+                "mine_tgt_xyz args");
+  return mine_tgt_xyz(xyz_src, pose, n_planes, batch, h, w, xyz_tgt, (hipStream_t)stream);
+}
+int md2_mine_sample(const float* src, int c, const float* depth, const float* pose, int n_planes,
+                    int batch, int h, int w, const float* K, const float* invK, float* out,
+                    float* valid, void* stream) {
+  MD2_CHECK_ARG(src && depth && pose && K && invK && out && valid && c > 0 && n_planes > 0 &&
+                    batch > 0 && h >= 2 && w >= 2, "mine_sample args (h, w >= 2)");
+  return mine_sample(src, c, depth, pose, n_planes, batch, h, w, mat3(K), mat3(invK), out, valid,
+                     (hipStream_t)stream);
+}
+int md2_plane_volume_rendering(const float* rgb, const float* sigma, const float* xyz, int n_planes,
+                               int batch, int h, int w, float* rgb_out, float* transparency_acc,
+                               float* weights, void* stream) {
+  MD2_CHECK_ARG(rgb && sigma && xyz && rgb_out && transparency_acc && weights && n_planes > 0 &&
+                    batch > 0 && h > 0 && w > 0, "plane_volume_rendering args");
+  return plane_volume_rendering(rgb, sigma, xyz, n_planes, batch, h, w, rgb_out, transparency_acc,
+                                weights, (hipStream_t)stream);
+}
+int md2_render_tgt_rgb_depth(const float* rgb, const float* sigma, const float* disparity,
+                             const float* xyz_tgt, const float* pose, const float* invK,
+                             const float* K, int n_planes, int batch, int h, int w, float* rgb_out,
+                             float* depth, float* mask, void* stream) {
+  MD2_CHECK_ARG(rgb && sigma && disparity && xyz_tgt && pose && invK && K && rgb_out && depth &&
+                    mask && n_planes > 0 && batch > 0 && h >= 2 && w >= 2,
+                "render_tgt_rgb_depth args (h, w >= 2)");
+  return render_tgt_rgb_depth(rgb, sigma, disparity, xyz_tgt, pose, mat3(invK), mat3(K), n_planes,
+                              batch, h, w, rgb_out, depth, mask, (hipStream_t)stream);
+}
 int md2_upsample2_bwd(const float* dy, int n, int c, int h, int w, float* dx, void* stream) {
   MD2_CHECK_ARG(dy && dx && n > 0 && c > 0 && h > 0 && w > 0, "upsample2_bwd args");
   return upsample2_bwd(dy, n, c, h, w, dx, (hipStream_t)stream);
@@ -274,7 +319,7 @@ static ArchCfg to_arch(const md2_model_cfg* c) {
 int md2_arch_param_count(const md2_model_cfg* cfg, long long* n_entries, long long* n_elems) {
   MD2_CHECK_ARG(cfg != nullptr, "cfg");
   MD2_CHECK_ARG(cfg->arch == 18 || cfg->arch == 34 || cfg->arch == 50, "arch 18/34/50");
-  MD2_CHECK_ARG(cfg->n_levels >= 1 && cfg->n_levels <= 4, "n_levels");
+  MD2_TRY(check_scale_levels(to_arch(cfg)));
   const auto t = build_param_table(to_arch(cfg));
   if (n_entries) *n_entries = (long long)t.size();
   if (n_elems) *n_elems = t.empty() ? 0 : (long long)(t.back().offset + t.back().numel);
@@ -284,6 +329,7 @@ int md2_arch_param_count(const md2_model_cfg* cfg, long long* n_entries, long lo
 int md2_arch_param_info(const md2_model_cfg* cfg, int idx, char* name, int name_len, int* ndim,
                         int* shape4, long long* offset) {
   MD2_CHECK_ARG(cfg != nullptr, "cfg");
+  MD2_TRY(check_scale_levels(to_arch(cfg)));
   const auto t = build_param_table(to_arch(cfg));
   MD2_CHECK_ARG(idx >= 0 && idx < (int)t.size(), "param index");
   const ParamEntry& e = t[idx];

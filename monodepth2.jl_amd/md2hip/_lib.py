@@ -120,6 +120,11 @@ _SIGS = {
     "md2_automasking_loss": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "md2_static_scores_workspace_size": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
     "md2_static_scores": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
+    "md2_mine_src_xyz": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
+    "md2_mine_tgt_xyz": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "md2_mine_sample": (C.c_int, [P, C.c_int, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P]),
+    "md2_plane_volume_rendering": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P]),
+    "md2_render_tgt_rgb_depth": (C.c_int, [P, P, P, P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P]),
     "md2_ssim_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "md2_ssim_bwd": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
     "md2_backproject_fwd": (C.c_int, [P, C.c_int, C.c_int, C.c_int, P, P, P]),

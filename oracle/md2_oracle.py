@@ -646,3 +646,100 @@ def slow_depth_init(width, height, dtype=torch.float64):
     rvecs = [torch.tensor([[0.0, 0.0, 0.01]], dtype=dtype) for _ in range(2)]
     tvecs = [torch.zeros(1, 3, dtype=dtype) for _ in range(2)]
     return disp, rvecs, tvecs
+
+
+# ------------------------------------------------------------------------------------------------
+# MINE plane rendering -- src/render.jl:21-114 (forward only upstream).  Layouts (C order, memory-
+# identical to the Julia arrays): rgb (W,H,3,N,B) <-> [B,N,3,H,W]; sigma (W,H,1,N,B) <->
+# [B,N,1,H,W]; xyz (3,W,H,N,B) <-> [B,N,H,W,3]; disparity (N,B) <-> [B,N]; Pose(rvec (3,B),
+# tvec (3,B)) <-> rvec [B,3], tvec [B,3]; sample's src (W,H,C,N*B) <-> [B*N,C,H,W].
+# Parity pins: the reference's MINE cross-check scripts (test/test_*.jl) compare against an
+# external PyTorch MINE checkout that is absent, so no reference outputs exist; the restatement
+# is pinned by analytic known answers of the reference formulas (tests/test_mine_oracle.py).
+# ------------------------------------------------------------------------------------------------
+def create_meshgrid(H: int, W: int, dtype=torch.float64):
+    """``create_meshgrid(H, W)`` -- src/render.jl:21-23: (3,W,H) of 1-based (w, h, 1) <->
+    [H,W,3]."""
+    w = torch.arange(1, W + 1, dtype=dtype).view(1, W).expand(H, W)
+    h = torch.arange(1, H + 1, dtype=dtype).view(H, 1).expand(H, W)
+    return torch.stack([w, h, torch.ones(H, W, dtype=dtype)], -1)
+
+
+def get_src_xyz_from_plane_disparity(meshgrid, disparity, invK):
+    """src/render.jl:25-30: K^-1 [w, h, 1] / disparity[n, b].  meshgrid [H,W,3], disparity
+    [B,N] -> [B,N,H,W,3]."""
+    rays = meshgrid @ invK.T                                  # [H,W,3]
+    return rays.view(1, 1, *rays.shape) * (1.0 / disparity).view(*disparity.shape, 1, 1, 1)
+
+
+def plane_volume_rendering(rgb, sigma, xyz):
+    """src/render.jl:32-49.  rgb [B,N,3,H,W], sigma [B,N,1,H,W], xyz [B,N,H,W,3] ->
+    rgb_out [B,3,H,W], transparency_acc [B,N,1,H,W], weights [B,N,1,H,W]."""
+    B, N, _, H, W = rgb.shape
+    diff = xyz[:, 1:] - xyz[:, :-1]                           # [B,N-1,H,W,3]
+    dist = torch.sqrt((diff * diff).sum(-1)).unsqueeze(2)     # [B,N-1,1,H,W]
+    dist = torch.cat([dist, torch.full((B, 1, 1, H, W), 1e3, dtype=rgb.dtype)], 1)
+    transparency = torch.exp(-dist * sigma)
+    alpha = 1 - transparency
+    acc = torch.cumprod(transparency + 1e-6, 1)
+    acc = torch.cat([torch.ones(B, 1, 1, H, W, dtype=rgb.dtype), acc[:, :-1]], 1)
+    weights = acc * alpha
+    return (weights * rgb).sum(1), acc, weights
+
+
+def get_tgt_xyz_from_plane_disparity(xyz_src, rvec, tvec):
+    """src/render.jl:51-64: R(rvec_b) xyz + t_b.  xyz_src [B,N,H,W,3] -> [B,N,H,W,3]."""
+    R = so3_exp_map(rvec)                                     # [B,3,3]
+    return torch.einsum("bij,bnhwj->bnhwi", R, xyz_src) + tvec.view(-1, 1, 1, 1, 3)
+
+
+def mine_homographies(depth, rvec, tvec, K, invK):
+    """H_src_tgt of ``sample`` (src/render.jl:68-79): inv(K (R - t n^T / (-d)) K^-1), n = (0,0,1).
+    depth [B,N] -> [B*N,3,3] (q = b*N + n)."""
+    B, N = depth.shape
+    R = so3_exp_map(rvec)                                     # [B,3,3]
+    n = torch.tensor([[0.0, 0.0, 1.0]], dtype=depth.dtype)
+    tn = tvec.unsqueeze(-1) @ n                               # [B,3,3] = t n^T
+    temp = tn.unsqueeze(1) / (-depth).view(B, N, 1, 1)        # [B,N,3,3]
+    Ht = K @ (R.unsqueeze(1) - temp).reshape(B * N, 3, 3) @ invK
+    return torch.linalg.inv(Ht)
+
+
+def mine_sample(src, depth, rvec, tvec, K, invK, return_coords=False):
+    """``sample(src, depth_src, pose, K, K_inv)`` -- src/render.jl:66-94, as written: the valid
+    mask is Julia's chained comparison ``u .< W .* u .>= 0`` = (u < W u) & (W u >= 0), and the
+    grid is (u + 0.5)/(W/2) with no -1 shift, then grid_sample(:border, align_corners).
+    src [B*N,C,H,W], depth [B,N] -> tgt [B*N,C,H,W], valid [B*N, H*W] (bool)."""
+    BN, C, H, W = src.shape
+    Hst = mine_homographies(depth, rvec, tvec, K, invK)      # [BN,3,3]
+    mg = create_meshgrid(H, W, src.dtype).reshape(H * W, 3) - torch.tensor([1.0, 1.0, 0.0], dtype=src.dtype)
+    m = torch.einsum("qij,pj->qip", Hst, mg)                  # [BN,3,HW]
+    a2 = m[:, 2]
+    u, v = m[:, 0] / a2, m[:, 1] / a2
+    valid = (u < W * u) & (W * u >= 0) & (v < H * v) & (H * v >= 0)
+    gx = (u + 0.5) / (W / 2)
+    gy = (v + 0.5) / (H / 2)
+    grid = torch.stack([gx, gy], -1).view(BN, H, W, 2)
+    tgt = grid_sample_border(src, grid)
+    if return_coords:
+        return tgt, valid, (u, v, a2)
+    return tgt, valid
+
+
+def render_tgt_rgb_depth(rgb, sigma, disparity, xyz_tgt, rvec, tvec, invK, K, return_coords=False):
+    """src/render.jl:96-114.  rgb [B,N,3,H,W], sigma [B,N,1,H,W], disparity [B,N], xyz_tgt
+    [B,N,H,W,3] -> rgb [B,3,H,W], depth (= transparency_acc) [B,N,1,H,W], mask [B,1,H,W] (the
+    per-pixel count of valid planes)."""
+    B, N, _, H, W = rgb.shape
+    depth_src = 1.0 / disparity
+    packed = torch.cat([rgb, sigma, xyz_tgt.permute(0, 1, 4, 2, 3)], 2).reshape(B * N, 7, H, W)
+    out = mine_sample(packed, depth_src, rvec, tvec, K, invK, return_coords=True)
+    tgt, valid, coords = out
+    tgt = tgt.view(B, N, 7, H, W)
+    s = tgt[:, :, 3:4]
+    s = s * (s >= 0)
+    rgb_out, acc, _ = plane_volume_rendering(tgt[:, :, 0:3], s, tgt[:, :, 4:7].permute(0, 1, 3, 4, 2))
+    mask = valid.view(B, N, 1, H, W).sum(1).to(rgb.dtype)
+    if return_coords:
+        return rgb_out, acc, mask, coords
+    return rgb_out, acc, mask
