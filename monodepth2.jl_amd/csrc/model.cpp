@@ -245,6 +245,12 @@ class Model {
   RConv sq, p1, p2, p3;
   float *sqo = nullptr, *pc1 = nullptr, *pc2 = nullptr, *means = nullptr, *pose = nullptr;
   float *d_pose = nullptr, *d_pc1 = nullptr, *d_pin = nullptr, *d_sq = nullptr;
+  // pose pair j of sample q = frames (pa[j], pb[j]) (src/model.jl:57-70); the default (target 2,
+  // sources 1, 3) pairs are images (q, q+N) and read sqo in place, other ids gather into pin
+  int pa[2] = {0, 1}, pb[2] = {1, 2};
+  bool pairs_inplace = true;
+  float* pin = nullptr;
+  int T0 = 0;                   // image offset of the target frame's slice (target * N)
   // scratch
   float *DA = nullptr, *DY = nullptr, *G = nullptr, *DYD = nullptr;
   float *DPRE = nullptr, *DUP = nullptr, *DO1 = nullptr;
@@ -446,6 +452,14 @@ class Model {
     MD2_TRY(alloc(&d_pc1, 2L * N * 256 * hw4));
     MD2_TRY(alloc(&pc2, 2L * N * 256 * hw4));
     MD2_TRY(alloc(&d_pin, 2L * N * 512 * hw4));
+    for (int j = 0; j < 2; ++j) {
+      const int s = j ? cfg.src1 : cfg.src0;
+      pa[j] = std::min(s, cfg.target);
+      pb[j] = std::max(s, cfg.target);
+    }
+    pairs_inplace = pa[0] == 0 && pa[1] == 1 && pb[0] == 1 && pb[1] == 2;
+    if (!pairs_inplace) MD2_TRY(alloc(&pin, 2L * N * 512 * hw4));
+    T0 = cfg.target * N;
     MD2_TRY(alloc(&means, 2L * N * 256));
     MD2_TRY(alloc(&pose, 2L * N * 6));
     MD2_TRY(alloc(&d_pose, 2L * N * 6));
@@ -704,13 +718,20 @@ class Model {
     return MD2_OK;
   }
 
-  int pose_fwd(hipStream_t st) {
-    const long hw4 = (long)featH[4] * featW[4];
-    MD2_TRY(conv_f(sq, B, tin(feat[4], featC[4], hw4), sqo, 256 * hw4, ACT_RELU, 0, st));
+  // PoseDecoder input of the 2N pairs: in place for the default ids, else the gathered pin
+  TensorIn pose_pairs_in(long hw4) {
+    if (!pairs_inplace) return tin(pin, 512, hw4);
     TensorIn in = tin(sqo, 256, hw4);
     in.p1 = sqo + (long)N * 256 * hw4;   // pair (frame s, frame s+1) = images (q, q+N)
     in.bs1 = 256 * hw4;
-    MD2_TRY(conv_f(p1, 2 * N, in, pc1, 256 * hw4, ACT_RELU, 0, st));
+    return in;
+  }
+
+  int pose_fwd(hipStream_t st) {
+    const long hw4 = (long)featH[4] * featW[4];
+    MD2_TRY(conv_f(sq, B, tin(feat[4], featC[4], hw4), sqo, 256 * hw4, ACT_RELU, 0, st));
+    if (!pairs_inplace) MD2_TRY(pair_gather(sqo, N, 256, hw4, pa, pb, pin, st));
+    MD2_TRY(conv_f(p1, 2 * N, pose_pairs_in(hw4), pc1, 256 * hw4, ACT_RELU, 0, st));
     MD2_TRY(conv_f(p2, 2 * N, tin(pc1, 256, hw4), pc2, 256 * hw4, ACT_RELU, 0, st));
     return pose_head_fwd(pc2, 2 * N, 256, hw4, P(spec.p3.w), P(spec.p3.b), means, pose, st);
   }
@@ -725,7 +746,7 @@ class Model {
     in.bs0 = 3 * fs;
     in.bhi = fs;
     MD2_TRY(encoder_fwd(in, B, st));
-    MD2_TRY(decoder_fwd(N, N, st));
+    MD2_TRY(decoder_fwd(N, T0, st));
     MD2_TRY(pose_fwd(st));
     const float* disps[MAX_SCALES] = {};
     LossTailOut o{};
@@ -899,11 +920,8 @@ class Model {
     MD2_TRY(act_bias(pc2, DPRE, DPRE, 2 * N, 256, hw4, ACT_RELU, st));
     MD2_TRY(conv_wd(p2, 2 * N, tin(pc1, 256, hw4), DPRE, d_pc1, 256 * hw4, 0, st));
     MD2_TRY(act_bias(pc1, d_pc1, d_pc1, 2 * N, 256, hw4, ACT_RELU, st));
-    TensorIn pin = tin(sqo, 256, hw4);
-    pin.p1 = sqo + (long)N * 256 * hw4;
-    pin.bs1 = 256 * hw4;
-    MD2_TRY(conv_wd(p1, 2 * N, pin, d_pc1, d_pin, 512 * hw4, 0, st));
-    MD2_TRY(pair_grad_gather(d_pin, N, 256, hw4, d_sq, st));
+    MD2_TRY(conv_wd(p1, 2 * N, pose_pairs_in(hw4), d_pc1, d_pin, 512 * hw4, 0, st));
+    MD2_TRY(pair_grad_gather(d_pin, N, 256, hw4, pa, pb, d_sq, st));
     MD2_TRY(act_bias(sqo, d_sq, d_sq, B, 256, hw4, ACT_RELU, st));
     float* d_f4 = stages[3].back().d_out;
     MD2_TRY(conv_wd(sq, B, tin(feat[4], featC[4], hw4), d_sq, d_f4, (long)featC[4] * hw4, 0, st));
@@ -922,7 +940,7 @@ class Model {
       long skip_bs = 0;
       if (d.b.cskip > 0) {
         const int fi = 4 - d.b.bid;
-        in.p1 = feat[fi] + (long)N * featC[fi] * hw2;
+        in.p1 = feat[fi] + (long)T0 * featC[fi] * hw2;
         in.bs1 = (long)featC[fi] * hw2;
         dskip = d_skip[fi];
         skip_bs = (long)featC[fi] * hw2;
@@ -936,8 +954,8 @@ class Model {
       int acc;
       if (i == 0) {
         cin = featC[4];
-        xin = feat[4] + (long)N * cin * hw;
-        dx = d_f4 + (long)N * cin * hw;
+        xin = feat[4] + (long)T0 * cin * hw;
+        dx = d_f4 + (long)T0 * cin * hw;
         acc = 1;
       } else {
         cin = br[i - 1].b.cout;
@@ -956,7 +974,7 @@ class Model {
     if (si >= 1) {
       // d f_si (= block 0's d_in) += decoder skip gradient on the target slice
       const long n = (long)N * featC[si] * featH[si] * featW[si];
-      MD2_TRY(axpy(sg[0].d_in + n, d_skip[si], n, st));
+      MD2_TRY(axpy(sg[0].d_in + (long)T0 * featC[si] * featH[si] * featW[si], d_skip[si], n, st));
     }
     return MD2_OK;
   }
@@ -965,7 +983,7 @@ class Model {
     const long hw0 = (long)H0 * W0;
     MD2_TRY(maxpool_bwd(d_mp, mp_arg, B, 64, H0, W0, Hm, Wm, d_f0, st));
     const long n = (long)N * 64 * hw0;
-    MD2_TRY(axpy(d_f0 + n, d_skip[0], n, st));
+    MD2_TRY(axpy(d_f0 + (long)T0 * 64 * hw0, d_skip[0], n, st));
     MD2_TRY(bn_bwd(stem_bn, d_f0, f0, y0, B, hw0, DY, nullptr, 0, st));
     const long fs = (long)cfg.arch.in_ch * cfg.H * cfg.W;
     TensorIn in;
@@ -982,20 +1000,34 @@ class Model {
 };
 
 // ---------------------------------------------------------------------------------------------
+// DepthDecoder(; scale_levels) (src/depth_decoder.jl:26-50): at most 5 levels in 1:5 (the
+// reference's own error); levels that do not strictly increase are MD2_ENOTSUP (the reference
+// then builds empty branches: a duplicate head for a repeated level, a channel mismatch at run
+// time for a decreasing one)
+int check_scale_levels(const ArchCfg& a) {
+  MD2_CHECK_ARG(a.nlevels >= 1 && a.nlevels <= MAX_SCALES,
+                "`scale_levels` should be at most of length 5 and have values in [1, 5] range.");
+  for (int i = 0; i < a.nlevels; ++i)
+    MD2_CHECK_ARG(a.levels[i] >= 1 && a.levels[i] <= 5,
+                  "`scale_levels` should be at most of length 5 and have values in [1, 5] range.");
+  for (int i = 1; i < a.nlevels; ++i)
+    if (a.levels[i] <= a.levels[i - 1]) {
+      set_error("scale_levels must be strictly increasing (repeated / decreasing levels: not supported)");
+      return MD2_ENOTSUP;
+    }
+  return MD2_OK;
+}
+
 int model_create(const ModelCfg& cfg, float* params, float* grads, Model** out) {
   MD2_CHECK_ARG(out != nullptr && params != nullptr && grads != nullptr, "model_create args");
   MD2_CHECK_ARG(cfg.arch.arch == 18 || cfg.arch.arch == 34 || cfg.arch.arch == 50, "arch 18/34/50");
   MD2_CHECK_ARG(cfg.arch.in_ch == 1 || cfg.arch.in_ch == 3, "in_channels 1 or 3");
   MD2_CHECK_ARG(cfg.N >= 1 && cfg.W % 32 == 0 && cfg.H % 32 == 0 && cfg.W >= 64 && cfg.H >= 64,
                 "width/height must be multiples of 32 (>= 64)");
-  MD2_CHECK_ARG(cfg.target == 1 && cfg.src0 == 0 && cfg.src1 == 2,
-                "the HIP model supports target_id=2, source_ids=[1,3] (Depth10k/KITTI triplets)");
-  MD2_CHECK_ARG(cfg.arch.nlevels >= 1 && cfg.arch.nlevels <= 4, "scale levels");
-  for (int i = 0; i < cfg.arch.nlevels; ++i)
-    MD2_CHECK_ARG(cfg.arch.levels[i] >= 2 && cfg.arch.levels[i] <= 5 &&
-                      (i == 0 || cfg.arch.levels[i] > cfg.arch.levels[i - 1]),
-                  "scale_levels must be increasing in 2:5");
-  MD2_CHECK_ARG(cfg.arch.levels[cfg.arch.nlevels - 1] == 5, "the last scale level must be 5 (full res)");
+  // TrainCache(target_id, source_ids) over triplets (src/Monodepth.jl:49-60): any frames of 3
+  MD2_CHECK_ARG(cfg.target >= 0 && cfg.target < 3 && cfg.src0 >= 0 && cfg.src0 < 3 && cfg.src1 >= 0 &&
+                    cfg.src1 < 3, "target / source ids must be frames of the triplet (1-based 1:3)");
+  MD2_TRY(check_scale_levels(cfg.arch));
   Model* m = new Model();
   m->cfg = cfg;
   m->params = params;

@@ -49,6 +49,9 @@ int model_profile_read(Model* m, double* out, int ncat);
 int model_profile_records(Model* m, int max, double* ms, double* work, int* cat, char* tags,
                           int tag_len, int* count);
 int model_create(const ModelCfg& cfg, float* params, float* grads, Model** out);
+// scale_levels validation shared by the parameter table and the executor (MD2_ENOTSUP for
+// non-increasing levels)
+int check_scale_levels(const ArchCfg& a);
 void model_destroy(Model* m);
 
 // train path

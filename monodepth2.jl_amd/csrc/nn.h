@@ -87,7 +87,11 @@ int pose_head_bwd(const float* dpose, int Q, int C, long HW, const float* w, con
 
 // ---- misc elementwise ----
 int axpy(float* y, const float* x, long n, hipStream_t st);               // y += x
-int pair_grad_gather(const float* dpin, int N, int C, long HW, float* dsq, hipStream_t st);
+// pose pairs (a_j, b_j) of frames: PoseDecoder input gather / its gradient scatter (nn.hip)
+int pair_gather(const float* sq, int N, int C, long HW, const int a[2], const int b[2], float* pin,
+                hipStream_t st);
+int pair_grad_gather(const float* dpin, int N, int C, long HW, const int a[2], const int b[2],
+                     float* dsq, hipStream_t st);
 
 // ---- Flux ADAM over the flat parameter vector ----
 int adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,

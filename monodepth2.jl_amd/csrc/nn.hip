@@ -976,26 +976,59 @@ int axpy(float* y, const float* x, long n, hipStream_t st) {
 
 // pose pairs q = s*N + n read (sq[q], sq[q+N]) (src/model.jl:65-70 in frame-major order):
 // dsq[b] = (b < 2N ? dpin[b][0:C] : 0) + (b >= N ? dpin[b-N][C:2C] : 0)
+// Pose pairs (src/model.jl:57-70 _get_pose_features): pair j of sample q = (frame a_j, frame b_j)
+// with a_j = min(source_j, target), b_j = max(source_j, target); squeezer outputs are frame-major
+// images f*N + q.  pair_gather builds the PoseDecoder input [2N][2C][HW] (only when the pairs are
+// not the (q, q+N) zero-copy layout of target 2 / sources 1, 3); pair_grad scatters its gradient
+// back: d sq[f*N + q] = sum_j [a_j == f] d pin[jN + q][:C] + [b_j == f] d pin[jN + q][C:].
+__global__ __launch_bounds__(256) void pair_gather_kernel(const float* __restrict__ sq, int N,
+                                                          FastDiv fdper, int a0, int a1, int b0,
+                                                          int b1, float* __restrict__ pin,
+                                                          uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;   // over [2N][2][per]
+  if (i >= n) return;
+  const long per = fdper.d;
+  const uint32_t row = fdiv(i, fdper);                // (jN + q)*2 + half
+  const long r = i - (long)row * per;
+  const int half = row & 1, img = row >> 1, j = img >= N ? 1 : 0, q = img - j * N;
+  const int f = half ? (j ? b1 : b0) : (j ? a1 : a0);
+  pin[i] = sq[((long)f * N + q) * per + r];
+}
+
 __global__ __launch_bounds__(256) void pair_grad_kernel(const float* __restrict__ dpin, int N,
-                                                        FastDiv fdper, float* __restrict__ dsq,
+                                                        FastDiv fdper, int a0, int a1, int b0,
+                                                        int b1, float* __restrict__ dsq,
                                                         uint32_t n) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;   // over [3N][per]
   if (i >= n) return;
   const long per = fdper.d;
   const uint32_t b = fdiv(i, fdper);
   const long r = i - (long)b * per;
+  const int f = (int)b / N, q = (int)b - f * N;
   float s = 0.f;
-  const long bl = b;
-  if (bl < 2L * N) s += dpin[bl * 2 * per + r];
-  if (bl >= N) s += dpin[(bl - N) * 2 * per + per + r];
+  if (a0 == f) s += dpin[((long)q * 2) * per + r];
+  if (b0 == f) s += dpin[((long)q * 2 + 1) * per + r];
+  if (a1 == f) s += dpin[((long)(N + q) * 2) * per + r];
+  if (b1 == f) s += dpin[((long)(N + q) * 2 + 1) * per + r];
   dsq[i] = s;
 }
 
-int pair_grad_gather(const float* dpin, int N, int C, long HW, float* dsq, hipStream_t st) {
+int pair_gather(const float* sq, int N, int C, long HW, const int a[2], const int b[2], float* pin,
+                hipStream_t st) {
+  const long n = 4L * N * C * HW;
+  MD2_TRY(check_u31(n));
+  hipLaunchKernelGGL(pair_gather_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, sq, N, fd((long)C * HW),
+                     a[0], a[1], b[0], b[1], pin, (uint32_t)n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int pair_grad_gather(const float* dpin, int N, int C, long HW, const int a[2], const int b[2],
+                     float* dsq, hipStream_t st) {
   const long n = 3L * N * C * HW;
   MD2_TRY(check_u31(2 * n));
   hipLaunchKernelGGL(pair_grad_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dpin, N, fd((long)C * HW),
-                     dsq, (uint32_t)n);
+                     a[0], a[1], b[0], b[1], dsq, (uint32_t)n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }

@@ -51,8 +51,10 @@ class DepthDecoder:
             # defects D2/D4: the MPI-embedding decoder is forward-only upstream
             raise NotImplementedError("the HIP train step runs the mono DepthDecoder (embedding_levels=0); "
                                       "MPI mode (forward only, as upstream): md2hip.MPIDepthDecoder + md2hip.mpi_forward")
-        if levels != sorted(set(levels)) or levels[-1] != 5 or levels[0] < 2:
-            raise NotImplementedError("HIP DepthDecoder supports increasing scale_levels in 2:5 ending at 5")
+        if any(b <= a for a, b in zip(levels, levels[1:])):
+            # the reference builds an empty branch here: a duplicate head for a repeated level, a
+            # channel mismatch at run time for a decreasing one (library: MD2_ENOTSUP)
+            raise NotImplementedError("scale_levels must be strictly increasing")
         self.encoder_channels = tuple(encoder_channels)
         self.scale_levels = tuple(levels)
         self.embedding_levels = embedding_levels
@@ -86,8 +88,13 @@ def _cfg(arch, in_ch, levels, batch=1, width=64, height=64, cache: Optional[Trai
             c.K[i], c.invK[i] = float(K[i]), float(iK[i])
         for i, s in enumerate(cache.scales):
             c.scales[i] = float(s)
-        if tuple(cache.source_ids) != (1, 3) or cache.target_id != 2:
-            raise NotImplementedError("HIP model supports target_id=2, source_ids=[1,3]")
+        ids = (cache.target_id, *cache.source_ids)
+        if len(cache.source_ids) != 2:
+            raise NotImplementedError("the HIP model takes exactly two source frames (TrainCache.source_ids)")
+        if any(not 1 <= i <= 3 for i in ids):
+            raise ValueError("target_id / source_ids must be frames of the triplet (1:3)")
+        if len(cache.scales) != len(levels):
+            raise ValueError("TrainCache.scales must have one entry per DepthDecoder scale level")
         c.target, c.src0, c.src1 = cache.target_id - 1, cache.source_ids[0] - 1, cache.source_ids[1] - 1
     if params is not None:
         c.min_depth, c.max_depth = params.min_depth, params.max_depth

@@ -7,14 +7,20 @@ from oracle import md2_oracle as O
 from tests import _data as D
 
 
-def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, automasking=False):
+DEFAULT_SCALES = {1: 0.0625, 2: 0.125, 3: 0.25, 4: 0.5, 5: 1.0}
+
+
+def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, automasking=False, levels=(2, 3, 4, 5),
+        target_id=2, source_ids=(1, 3)):
     x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
     K, invK = D.intrinsics(W, H)
     enc = md2hip.ResNet(arch, in_channels=C)
-    model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
+    model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=list(levels),
                                                   embedding_levels=0),
                          md2hip.PoseDecoder(enc.stages[-1]), seed=42)
-    cache = md2hip.TrainCache(K=K.numpy(), invK=invK.numpy())
+    scales = tuple(DEFAULT_SCALES[l] for l in levels)
+    cache = md2hip.TrainCache(K=K.numpy(), invK=invK.numpy(), target_id=target_id,
+                              source_ids=tuple(source_ids), scales=scales)
     params = md2hip.Params(target_size=(W, H), batch_size=N, automasking=automasking)
     xg = x.float().cuda().contiguous()
     loss, *_ = md2hip.train_loss(model, xg, None, cache, params)
@@ -27,17 +33,17 @@ def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, automasking=False):
     g = {"loss": loss.item(), "tail_loss": tail["loss"].item(), "disps": [d.cpu() for d in disps],
          "pose": pose.cpu(), "grad": model.grad.cpu(), "sel": tail["vis_sel"].cpu(),
          "flat": model.flat.detach().double().cpu()}
-    g["decisions"] = gpu_decisions(model, N, arch)
-    spec = O.param_spec(arch, C, (2, 3, 4, 5))
+    g["decisions"] = gpu_decisions(model, N, arch, target_id=target_id, source_ids=source_ids)
+    spec = O.param_spec(arch, C, tuple(levels))
     flat = model.flat.detach().double().cpu().clone().requires_grad_(True)
     P = O.unflatten(flat, spec)
     with O.forced_decisions(g["decisions"]):
-        d_o, p_o = O.model_forward(P, x, arch=arch)
-    cache_o = O.TrainCache(K=K, invK=invK)
+        d_o, p_o = O.model_forward(P, x, source_ids, target_id, arch=arch, scale_levels=tuple(levels))
+    cache_o = O.TrainCache(K=K, invK=invK, target_id=target_id, source_ids=tuple(source_ids), scales=scales)
     par_o = O.Params(target_size=(W, H), batch_size=N, automasking=automasking)
     # the GPU's argmin (-1 = automask) as an index into [auto_loss?, source 0, source 1]
-    forced = [g["sel"][s].unsqueeze(1).long() + (1 if automasking else 0) for s in range(4)]
-    auto_o = O.automasking_loss(x, x[:, 1], (1, 3)) if automasking else None
+    forced = [g["sel"][s].unsqueeze(1).long() + (1 if automasking else 0) for s in range(len(levels))]
+    auto_o = O.automasking_loss(x, x[:, target_id - 1], source_ids) if automasking else None
     loss_o = O.loss_from_outputs(d_o, p_o, x, auto_o, cache_o, par_o, forced_sel=forced)
     loss_o.backward()
     o = {"loss": loss_o.item(), "disps": [d.detach() for d in d_o],
@@ -55,7 +61,7 @@ def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, automasking=False):
     return g, o, errs
 
 
-def gpu_decisions(model, N, arch=18, L=3):
+def gpu_decisions(model, N, arch=18, L=3, target_id=2, source_ids=(1, 3)):
     """The GPU forward's branch decisions (ReLU masks, max-pool argmax) in the oracle's layout
     (encoder batch n-major; pose per source pair) for O.forced_decisions."""
     from oracle import md2_oracle as O
@@ -72,10 +78,11 @@ def gpu_decisions(model, N, arch=18, L=3):
             for r in ("relu1", "relu2"):           # BasicBlock: relu1; Bottleneck: relu1, relu2
                 if f"{q}.{r}" in t:
                     d[f"encoder.{q}.{r}"] = nmajor(t[f"{q}.{r}"] > 0)
-    sq = t["pose.sq"] > 0
-    for j in range(2):                       # pair j = frames (j, j+1), GPU pairs [jN, (j+1)N)
-        d[f"pose{j}.sqa"] = sq[j * N:(j + 1) * N]
-        d[f"pose{j}.sqb"] = sq[(j + 1) * N:(j + 2) * N]
+    sq = t["pose.sq"] > 0                    # squeezer outputs of the 3N frame-major images
+    for j, s in enumerate(source_ids):       # pair j = frames (min(s,t), max(s,t)), GPU rows [jN, (j+1)N)
+        a, b = min(s, target_id) - 1, max(s, target_id) - 1
+        d[f"pose{j}.sqa"] = sq[a * N:(a + 1) * N]
+        d[f"pose{j}.sqb"] = sq[b * N:(b + 1) * N]
         d[f"pose{j}.conv1"] = t["pose.conv1"][j * N:(j + 1) * N] > 0
         d[f"pose{j}.conv2"] = t["pose.conv2"][j * N:(j + 1) * N] > 0
     return d
@@ -108,24 +115,29 @@ def oracle_at_gpu_outputs(g, N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7
 
 
 def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=None, sel=None,
-                      decisions=None):
+                      decisions=None, levels=(2, 3, 4, 5), target_id=2, source_ids=(1, 3)):
     """Per-tensor gradient error of the SAME oracle run in fp32 vs fp64 (the fp32 noise floor),
     plus the forward outputs' floors under the keys "__disp<s>" and "__pose"."""
     x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
     K, invK = D.intrinsics(W, H)
-    spec = O.param_spec(arch, C, (2, 3, 4, 5))
-    grads, fwd = [], []
+    spec = O.param_spec(arch, C, tuple(levels))
+    scales = tuple(DEFAULT_SCALES[l] for l in levels)
+    grads, fwd, losses = [], [], []
     for dt in (torch.float64, torch.float32):
         f = flat.to(dt).clone().requires_grad_(True)
         P = O.unflatten(f, spec)
         with O.forced_decisions(decisions or {}):
-            d_o, p_o = O.model_forward(P, x.to(dt), arch=arch)
+            d_o, p_o = O.model_forward(P, x.to(dt), source_ids, target_id, arch=arch,
+                                       scale_levels=tuple(levels))
         fwd.append(([d.detach().double() for d in d_o],
                     torch.cat([torch.cat([r, t], 1) for r, t in p_o], 0).detach().double()))
-        cache_o = O.TrainCache(K=K.to(dt), invK=invK.to(dt))
+        cache_o = O.TrainCache(K=K.to(dt), invK=invK.to(dt), target_id=target_id,
+                               source_ids=tuple(source_ids), scales=scales)
         par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
         forced = [s.unsqueeze(1).long() for s in sel]
-        O.loss_from_outputs(d_o, p_o, x.to(dt), None, cache_o, par_o, forced_sel=forced).backward()
+        lo = O.loss_from_outputs(d_o, p_o, x.to(dt), None, cache_o, par_o, forced_sel=forced)
+        lo.backward()
+        losses.append(lo.item())
         grads.append(f.grad.double())
     errs, off = {}, 0
     for name, shape in spec:
@@ -138,4 +150,5 @@ def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=
     for s_, (a, b) in enumerate(zip(fwd[1][0], fwd[0][0])):
         errs[f"__disp{s_}"] = D.rel_err(a, b)
     errs["__pose"] = D.rel_err(fwd[1][1], fwd[0][1])
+    errs["__loss"] = abs(losses[1] - losses[0]) / abs(losses[0])
     return errs

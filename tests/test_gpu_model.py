@@ -45,10 +45,33 @@ def test_model_train_loss_parity(arch, strict):
     assert not bad, bad
 
 
-def _flat(arch=18):
+@pytest.mark.parametrize("levels,target_id,source_ids", [((1, 3, 5), 1, (2, 3)), ((2, 4), 3, (1, 2)),
+                                                      ((1, 2, 3, 4, 5), 2, (3, 1))],
+                         ids=["levels135-target1", "levels24-target3", "levels12345-sources31"])
+def test_model_general_levels_and_frame_ids(levels, target_id, source_ids):
+    """Any strictly increasing scale_levels in 1:5 (src/depth_decoder.jl:26-50, incl. the 1/16
+    level 1 and a decoder that stops short of full resolution) and any target / two source frames
+    of the triplet (src/Monodepth.jl:49-60; pose pairs _get_pose_features, src/model.jl:64-69)."""
+    from tests._model_parity import oracle_fp32_floor, run
+    kw = dict(levels=levels, target_id=target_id, source_ids=source_ids)
+    g, o, errs = run(strict=True, **kw)
+    assert len(g["disps"]) == len(levels)
+    for l, d in zip(levels, g["disps"]):
+        assert d.shape[-2:] == (64 // 2 ** (5 - l), 128 // 2 ** (5 - l))
+    floor = oracle_fp32_floor(strict=True, flat=g["flat"], sel=[s for s in g["sel"]],
+                              decisions=g["decisions"], **kw)
+    assert abs(g["loss"] - o["loss"]) <= max(1e-6, 4 * floor["__loss"]) * abs(o["loss"]), floor["__loss"]
+    for s_, (a, b) in enumerate(zip(g["disps"], o["disps"])):
+        assert D.rel_err(a, b) < max(1e-5, 4 * floor[f"__disp{s_}"])
+    assert D.rel_err(g["pose"], o["pose"]) < max(1e-5, 4 * floor["__pose"])
+    bad = {k: (v, floor[k]) for k, v in errs.items() if v > max(4 * floor[k], 2e-4)}
+    assert not bad, bad
+
+
+def _flat(arch=18, levels=(2, 3, 4, 5)):
     import md2hip
     from md2hip.model import flux_init
-    table, total = md2hip.param_table(arch, 3, (2, 3, 4, 5))
+    table, total = md2hip.param_table(arch, 3, tuple(levels))
     return flux_init(table, total, seed=42).float().double()
 
 

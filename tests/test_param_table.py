@@ -8,7 +8,8 @@ from oracle import md2_oracle as O
 
 
 @pytest.mark.parametrize("arch,in_ch,levels", [(18, 3, (2, 3, 4, 5)), (18, 1, (2, 3, 4, 5)),
-                                               (50, 3, (2, 3, 4, 5)), (34, 3, (3, 5))])
+                                               (50, 3, (2, 3, 4, 5)), (34, 3, (3, 5)),
+                                               (18, 3, (1, 2, 3, 4, 5)), (18, 3, (1, 3)), (18, 3, (4,))])
 def test_param_table_matches_oracle(arch, in_ch, levels):
     import md2hip
     table, total = md2hip.param_table(arch, in_ch, levels)
@@ -39,3 +40,46 @@ def test_flux_init_matches_oracle():
     a = flux_init(table, total, seed=42)
     b = O.init_params(O.param_spec(18, 3, (2, 3, 4, 5)), seed=42)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("levels,rc", [((3, 3), 3), ((4, 2), 3), ((0, 5), 1), ((2, 6), 1),
+                                       ((1, 2, 3, 4, 5, 5), 1)])
+def test_rejected_scale_levels(levels, rc):
+    """Levels outside 1:5 or more than 5 of them: MD2_EINVAL (the reference's own error,
+    src/depth_decoder.jl:27-29); repeated / decreasing levels: MD2_ENOTSUP (the reference builds
+    empty branches: a duplicate head, or a channel mismatch at run time)."""
+    import ctypes as C
+    import md2hip
+    from md2hip._lib import ModelCfg, lib
+    c = ModelCfg()
+    c.arch, c.in_channels, c.n_levels = 18, 3, min(len(levels), 5)
+    for i, l in enumerate(levels[:5]):
+        c.scale_levels[i] = l
+    if len(levels) > 5:
+        c.n_levels = 6
+    n, e = C.c_longlong(), C.c_longlong()
+    assert lib().md2_arch_param_count(C.byref(c), C.byref(n), C.byref(e)) == rc
+    with pytest.raises(NotImplementedError if rc == 3 else ValueError):
+        md2hip.DepthDecoder(encoder_channels=(64, 64, 128, 256, 512), scale_levels=list(levels), embedding_levels=0)
+
+
+@pytest.mark.parametrize("target_id,source_ids,exc", [(4, (1, 3), ValueError), (2, (0, 3), ValueError),
+                                                      (2, (1,), NotImplementedError),
+                                                      (2, (1, 3, 3), NotImplementedError)])
+def test_rejected_frame_ids(target_id, source_ids, exc):
+    import md2hip
+    from md2hip.model import _cfg
+    K, iK = md2hip.depth10k_intrinsics(128, 64)
+    cache = md2hip.TrainCache(K=K, invK=iK, target_id=target_id, source_ids=source_ids)
+    with pytest.raises(exc):
+        _cfg(18, 3, (2, 3, 4, 5), cache=cache)
+
+
+def test_general_frame_ids_accepted():
+    import md2hip
+    from md2hip.model import _cfg
+    K, iK = md2hip.depth10k_intrinsics(128, 64)
+    for t, s in [(1, (2, 3)), (3, (1, 2)), (2, (3, 1))]:
+        c = _cfg(18, 3, (1, 3, 5), cache=md2hip.TrainCache(K=K, invK=iK, target_id=t, source_ids=s,
+                                                           scales=(0.0625, 0.25, 1.0)))
+        assert (c.target, c.src0, c.src1) == (t - 1, s[0] - 1, s[1] - 1)
