@@ -318,6 +318,13 @@ int md2_model_adam(md2_model* m, float* adam_m, float* adam_v, float lr, float b
 /* forward_loss + every backward segment + ADAM (single-GPU step) */
 int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, float* adam_m,
                          float* adam_v, float lr, int step, float* loss, void* stream);
+/* md2_model_train_step as ONE captured hipGraph (forward, loss, every backward segment, ADAM,
+ * weight repack): captured on the executor's own stream at the first call and again when adam_m,
+ * adam_v, lr or the presence of auto_loss change; x / auto_loss are copied into executor-owned
+ * buffers each call (any pointer may be passed), the loss is copied out; `step` may jump (the
+ * device step counter is re-set).  Same arithmetic, same results as md2_model_train_step. */
+int md2_model_train_step_graph(md2_model* m, const float* x, const float* auto_loss, float* adam_m,
+                               float* adam_v, float lr, int step, float* loss, void* stream);
 /* ------------------------------------------------------------------------------------------
  * Data parallelism over RCCL (xGMI), one process (rank) per GPU -- SURVEY.md 8(e).  The
  * reference has no collectives; these replace the torch.distributed plumbing so a Julia host

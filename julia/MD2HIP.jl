@@ -426,6 +426,17 @@ function find_static(dataset, α; batch=16)
     return keep
 end
 
+# One whole step (forward, loss, backward, ADAM(η) with β = (0.9, 0.999), ϵ = 1e-8) replayed as a
+# captured hipGraph; the same kernels in the same order as train_loss + gradient! + update!
+function train_step_graph!(m::HIPModel, x::ROCArray{Float32,5}, auto_loss, η)
+    m.step += 1; loss = ROCVector{Float32}(undef, 1)
+    check(ccall((:md2_model_train_step_graph, lib), Cint,
+                (Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Cfloat, Cint,
+                 Ptr{Float32}, Ptr{Cvoid}),
+                m.handle, x, ptr(auto_loss), m.m, m.v, η, m.step, loss, stream_ptr()))
+    return loss
+end
+
 # ------------------------------------------------------------------------------------------------
 # MINE plane rendering of the MPI mode (src/render.jl:21-114), forward only as upstream.  Same
 # names and argument order as the reference; `pose` is a Pose(rvec (3,B), tvec (3,B)) and goes to

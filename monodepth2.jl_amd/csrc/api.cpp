@@ -417,6 +417,13 @@ int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, f
   return model_adam(m->impl, adam_m, adam_v, lr, 0.9f, 0.999f, 1e-8f, step, 1.f, st);
 }
 
+int md2_model_train_step_graph(md2_model* m, const float* x, const float* auto_loss, float* adam_m,
+                               float* adam_v, float lr, int step, float* loss, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_train_step_graph(m->impl, x, auto_loss, adam_m, adam_v, lr, step, loss,
+                                (hipStream_t)stream);
+}
+
 int md2_model_set_profiling(md2_model* m, int on) {
   MD2_CHECK_ARG(m, "model");
   return model_set_profiling(m->impl, on);

@@ -264,9 +264,24 @@ class Model {
   const float* eval_disp[MAX_SCALES] = {};
 
   ~Model() {
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (g.st) (void)hipStreamDestroy(g.st);
     for (void* p : allocs) (void)hipFree(p);
     for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
   }
+
+  // graph-captured single-GPU step (model_train_step_graph): the executor owns the input copy,
+  // the loss slot and the device ADAM step counter, so one capture replays for every batch/step
+  struct StepGraph {
+    hipGraphExec_t exec = nullptr;
+    hipStream_t st = nullptr;
+    float *x = nullptr, *autoloss = nullptr, *loss = nullptr, *bc = nullptr;
+    int* step = nullptr;
+    float *adam_m = nullptr, *adam_v = nullptr;
+    float lr = 0.f;
+    int with_auto = -1;
+    int next_step = -1;
+  } g;
 
   int alloc(float** p, size_t n) {
     void* q = nullptr;
@@ -1051,6 +1066,86 @@ int model_forward_loss(Model* m, const float* x, const float* automask, float* l
 }
 
 int model_num_segments(Model* m) { return m ? 6 : 0; }
+
+// ---------------------------------------------------------------------------------------------
+// Graph-captured train step (forward + loss + every backward segment + ADAM + weight repack as
+// ONE hipGraph): the ~320 launches of a step replay without per-launch host work.  Captured on
+// the executor's own stream on first use (and again when adam_m / adam_v / lr / the automask
+// input change); each call copies x (and auto_loss) into the executor's input buffers, replays
+// on `st`, and copies the loss out.  ADAM's step count lives on the device (adam_prep), re-set
+// only when the caller's `step` is not the one the graph expects next.
+static int capture_step(Model* m, bool with_auto, float* adam_m, float* adam_v, float lr) {
+  auto& g = m->g;
+  if (g.exec) {
+    MD2_HIP(hipGraphExecDestroy(g.exec));
+    g.exec = nullptr;
+  }
+  if (!g.st) MD2_HIP(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
+  if (!g.x) {
+    const long xn = (long)m->N * 3 * m->cfg.arch.in_ch * m->cfg.H * m->cfg.W;
+    MD2_TRY(m->alloc(&g.x, xn));
+    MD2_TRY(m->alloc(&g.autoloss, (long)m->N * m->cfg.H * m->cfg.W));
+    MD2_TRY(m->alloc(&g.loss, 4));
+    MD2_TRY(m->alloc(&g.bc, 4));
+    float* q;
+    MD2_TRY(m->alloc(&q, 4));
+    g.step = (int*)q;
+  }
+  MD2_HIP(hipStreamBeginCapture(g.st, hipStreamCaptureModeThreadLocal));
+  auto body = [&]() -> int {
+    m->cur_x = g.x;
+    MD2_TRY(m->forward_loss(g.x, with_auto ? g.autoloss : nullptr, g.loss, nullptr, g.st));
+    for (int k = 0; k < model_num_segments(m); ++k) MD2_TRY(model_backward_segment(m, k, nullptr, nullptr, g.st));
+    MD2_TRY(adam_prep(g.step, g.bc, 0.9f, 0.999f, g.st));
+    MD2_TRY(adam_step_dev(m->params, m->grads, adam_m, adam_v, m->spec.total, lr, 0.9f, 0.999f, 1e-8f,
+                          g.bc, 1.f, g.st));
+    return m->repack(g.st);
+  };
+  const int rc = body();
+  hipGraph_t graph = nullptr;
+  const hipError_t e = hipStreamEndCapture(g.st, &graph);
+  if (rc) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  MD2_HIP(e);
+  const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  MD2_HIP(ei);
+  g.adam_m = adam_m;
+  g.adam_v = adam_v;
+  g.lr = lr;
+  g.with_auto = with_auto ? 1 : 0;
+  g.next_step = -1;
+  return MD2_OK;
+}
+
+int model_train_step_graph(Model* m, const float* x, const float* auto_loss, float* adam_m,
+                           float* adam_v, float lr, int step, float* loss, hipStream_t st) {
+  MD2_CHECK_ARG(m && x && adam_m && adam_v && loss && step >= 1, "train_step_graph args");
+  auto& g = m->g;
+  const bool with_auto = auto_loss != nullptr;
+  if (m->prof) {   // per-launch HIP events cannot live in a replayed graph: eager step
+    MD2_TRY(model_forward_loss(m, x, auto_loss, loss, nullptr, st));
+    for (int k = 0; k < model_num_segments(m); ++k) MD2_TRY(model_backward_segment(m, k, nullptr, nullptr, st));
+    return model_adam(m, adam_m, adam_v, lr, 0.9f, 0.999f, 1e-8f, step, 1.f, st);
+  }
+  if (!g.exec || g.adam_m != adam_m || g.adam_v != adam_v || g.lr != lr || g.with_auto != (int)with_auto)
+    MD2_TRY(capture_step(m, with_auto, adam_m, adam_v, lr));
+  const size_t xb = sizeof(float) * (size_t)m->N * 3 * m->cfg.arch.in_ch * m->cfg.H * m->cfg.W;
+  if (x != g.x) MD2_HIP(hipMemcpyAsync(g.x, x, xb, hipMemcpyDeviceToDevice, st));
+  if (with_auto)
+    MD2_HIP(hipMemcpyAsync(g.autoloss, auto_loss, sizeof(float) * (size_t)m->N * m->cfg.H * m->cfg.W,
+                           hipMemcpyDeviceToDevice, st));
+  if (step != g.next_step) MD2_TRY(set_device_int(g.step, step - 1, st));
+  MD2_HIP(hipGraphLaunch(g.exec, st));
+  MD2_HIP(hipMemcpyAsync(loss, g.loss, sizeof(float), hipMemcpyDeviceToDevice, st));
+  m->cur_x = g.x;
+  g.next_step = step + 1;
+  return MD2_OK;
+}
+
+
 
 int model_backward_segment(Model* m, int k, long* off, long* len, hipStream_t st) {
   MD2_CHECK_ARG(m && m->cur_x, "backward before forward");

@@ -64,6 +64,9 @@ int model_backward_segment(Model* m, int k, long* off, long* len, hipStream_t st
 int model_adam(Model* m, float* adam_m, float* adam_v, float lr, float b1, float b2, float eps,
                int step, float grad_scale, hipStream_t st);
 int model_repack(Model* m, hipStream_t st);   // after the parameters changed
+// forward + loss + backward + ADAM(0.9, 0.999, 1e-8) replayed as one captured hipGraph
+int model_train_step_graph(Model* m, const float* x, const float* auto_loss, float* adam_m,
+                           float* adam_v, float lr, int step, float* loss, hipStream_t st);
 // outputs of the last forward
 int model_outputs(Model* m, const float** disp, int* dw, int* dh, const float** pose);
 // the five encoder stage outputs of the last forward: [3N frame-major images][c][h][w]

@@ -94,6 +94,11 @@ int pair_grad_gather(const float* dpin, int N, int C, long HW, const int a[2], c
                      float* dsq, hipStream_t st);
 
 // ---- Flux ADAM over the flat parameter vector ----
+// graph-replayable ADAM: *step += 1 and bc = (1 - b1^t, 1 - b2^t) on the device, then the update
+int adam_prep(int* step, float* bc, float b1, float b2, hipStream_t st);
+int set_device_int(int* p, int v, hipStream_t st);
+int adam_step_dev(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
+                  float eps, const float* bc, float gscale, hipStream_t st);
 int adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
               float eps, float bc1, float bc2, float gscale, hipStream_t st);
 

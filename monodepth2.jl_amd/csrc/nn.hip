@@ -1049,6 +1049,55 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   p[i] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
 }
 
+// Graph-replayed ADAM: the step counter lives on the device (adam_prep increments it and forms
+// the bias corrections), so one captured step replays for every t.
+__global__ void adam_prep_kernel(int* __restrict__ step, float* __restrict__ bc, float b1, float b2) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int t = step[0] + 1;
+  step[0] = t;
+  bc[0] = (float)(1.0 - pow((double)b1, (double)t));
+  bc[1] = (float)(1.0 - pow((double)b2, (double)t));
+}
+
+__global__ void set_int_kernel(int* __restrict__ p, int v) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) p[0] = v;
+}
+
+__global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v, long n,
+                                                       float lr, float b1, float b2, float eps,
+                                                       const float* __restrict__ bc, float gscale) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float bc1 = bc[0], bc2 = bc[1];
+  const float gi = g[i] * gscale;
+  const float mi = b1 * m[i] + (1.f - b1) * gi;
+  const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  p[i] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+}
+
+int adam_prep(int* step, float* bc, float b1, float b2, hipStream_t st) {
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(64), 0, st, step, bc, b1, b2);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int set_device_int(int* p, int v, hipStream_t st) {
+  hipLaunchKernelGGL(set_int_kernel, dim3(1), dim3(64), 0, st, p, v);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int adam_step_dev(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
+                  float eps, const float* bc, float gscale, hipStream_t st) {
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, p, g, m, v, n, lr, b1, b2,
+                     eps, bc, gscale);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 int adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
               float eps, float bc1, float bc2, float gscale, hipStream_t st) {
   hipLaunchKernelGGL(adam_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, p, g, m, v, n, lr, b1, b2,

@@ -107,6 +107,7 @@ _SIGS = {
     "md2_model_backward_segment": (C.c_int, [P, C.c_int, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong), P]),
     "md2_model_adam": (C.c_int, [P, P, P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_float, P]),
     "md2_model_train_step": (C.c_int, [P, P, P, P, P, C.c_float, C.c_int, P, P]),
+    "md2_model_train_step_graph": (C.c_int, [P, P, P, P, P, C.c_float, C.c_int, P, P]),
     "md2_model_outputs": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.POINTER(C.c_void_p)]),
     "md2_model_eval_disparity": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_void_p), P]),

@@ -211,6 +211,29 @@ class _Executor:
         self.forwarded = True
         return loss
 
+    def train_step_graph(self, x, opt: "ADAM", auto_loss=None, loss=None):
+        """One full step (forward, loss, backward, Flux ADAM with opt's state) replayed as a
+        captured hipGraph (md2_model_train_step_graph): the same kernels in the same order as
+        forward_loss + backward + ADAM.update, without per-launch host work.  Returns the loss."""
+        import torch
+        if tuple(opt.beta) != (0.9, 0.999) or opt.eps != 1e-8:
+            raise NotImplementedError("the captured step uses ADAM's defaults beta=(0.9, 0.999), eps=1e-8")
+        loss = loss if loss is not None else torch.empty(1, dtype=torch.float32, device=x.device)
+        self.sync()
+        if opt.m is None:
+            opt.m = torch.zeros_like(self.model.flat)
+            opt.v = torch.zeros_like(self.model.flat)
+        am = auto_loss.contiguous() if (self.automask and auto_loss is not None) else None
+        opt.t += 1
+        check(lib().md2_model_train_step_graph(self.handle, ptr(x), ptr(am), ptr(opt.m), ptr(opt.v), opt.eta,
+                                               opt.t, ptr(loss), stream_of(x.device)),
+              "md2_model_train_step_graph")
+        self.forwarded = True
+        self.model._last = self
+        self.model.touch()
+        self.version = self.model.version
+        return loss
+
     def backward_segment(self, k):
         off, ln = C.c_longlong(), C.c_longlong()
         check(lib().md2_model_backward_segment(self.handle, k, C.byref(off), C.byref(ln),
