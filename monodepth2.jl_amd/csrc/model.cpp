@@ -891,13 +891,18 @@ class Model {
   }
   static constexpr long BP_WS = 8192;
 
+  // mask: the BN+ReLU output whose ReLU gates dout, or nullptr with relu_from_y for a residual-free
+  // BN+ReLU (stem, intra-block): the mask is re-derived from y (bit-exact, one read less)
   int bn_bwd(RBN& bn, const float* dout, const float* mask, const float* y, int nimg, long HW,
-             float* dy, float* dres, int dres_acc, hipStream_t st) {
+             float* dy, float* dres, int dres_acc, hipStream_t st, bool relu_from_y = false) {
     BNStatsWs w = bnws;
     w.parts = bn_parts(bn.p.c, nimg, HW);
-    MD2_TRY(bn_bwd_partial(dout, mask, y, bn.mean, bn.invstd, nimg, bn.p.c, HW, w, st));
+    const float* mg = relu_from_y ? P(bn.p.g) : nullptr;
+    const float* mb = relu_from_y ? P(bn.p.b) : nullptr;
+    if (relu_from_y) mask = nullptr;
+    MD2_TRY(bn_bwd_partial(dout, mask, y, bn.mean, bn.invstd, nimg, bn.p.c, HW, w, st, mg, mb));
     return bn_bwd_apply_fused(dout, mask, y, bn.mean, bn.invstd, P(bn.p.g), w, Gd(bn.p.g),
-                              Gd(bn.p.b), nimg, bn.p.c, HW, dy, dres, dres_acc, st);
+                              Gd(bn.p.b), nimg, bn.p.c, HW, dy, dres, dres_acc, st, mb);
   }
 
   int block_bwd(EncBlock& b, hipStream_t st) {
@@ -919,7 +924,7 @@ class Model {
       if (k > 0) {
         MD2_TRY(conv_wd(e.conv, nimg, tin(xin, cin, hin), DY, DA, (long)cin * hin, 0, st));
         EncStage& pe = b.st[k - 1];
-        MD2_TRY(bn_bwd(pe.bn, DA, pe.a, pe.y, nimg, hin, DY, nullptr, 0, st));
+        MD2_TRY(bn_bwd(pe.bn, DA, pe.a, pe.y, nimg, hin, DY, nullptr, 0, st, true));
       } else {
         MD2_TRY(conv_wd(e.conv, nimg, tin(xin, cin, hin), DY, b.d_in, (long)cin * hin, 1, st));
       }
@@ -999,7 +1004,7 @@ class Model {
     MD2_TRY(maxpool_bwd(d_mp, mp_arg, B, 64, H0, W0, Hm, Wm, d_f0, st));
     const long n = (long)N * 64 * hw0;
     MD2_TRY(axpy(d_f0 + (long)T0 * 64 * hw0, d_skip[0], n, st));
-    MD2_TRY(bn_bwd(stem_bn, d_f0, f0, y0, B, hw0, DY, nullptr, 0, st));
+    MD2_TRY(bn_bwd(stem_bn, d_f0, f0, y0, B, hw0, DY, nullptr, 0, st, true));
     const long fs = (long)cfg.arch.in_ch * cfg.H * cfg.W;
     TensorIn in;
     in.p0 = cur_x;

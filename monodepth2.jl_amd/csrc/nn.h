@@ -50,12 +50,15 @@ int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, cons
                   BNStatsWs ws, hipStream_t st);
 // backward partials only (bn_bwd_reduce without its finalise); bn_bwd_apply_fused then sums the
 // partials per block (dgamma/dbeta written once per channel) and applies -- model path
+// mgamma/mbeta non-null (and mask_out null): the ReLU mask of a residual-free BN+ReLU output is
+// re-derived from y bit-exactly (bn_apply_fused's explicit roundings) instead of read back
 int bn_bwd_partial(const float* dout, const float* mask_out, const float* y, const float* mean,
-                   const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st);
+                   const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st,
+                   const float* mgamma = nullptr, const float* mbeta = nullptr);
 int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y, const float* mean,
                        const float* invstd, const float* gamma, BNStatsWs ws, float* dgamma,
                        float* dbeta, int N, int C, long HW, float* dy, float* dres,
-                       int dres_accumulate, hipStream_t st);
+                       int dres_accumulate, hipStream_t st, const float* mbeta = nullptr);
 // dy = gamma*invstd*(g - dbeta/L - xhat*dgamma/L); optional dres (=g) store/accumulate
 int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const float* mean,
                  const float* invstd, const float* gamma, const float* dgamma,

@@ -33,17 +33,35 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
   const int U = VEC ? HW / 4 : HW;                 // units per image
   const uint32_t nu = (uint32_t)(i1 - i0) * U;
   double s = 0.0, ss = 0.0;
-  for (uint32_t e = threadIdx.x; e < nu; e += 256) {
-    const uint32_t im = fdiv(e, fdu), k = e - im * U;
-    const long base = ((long)(i0 + im) * C + c) * HW;
-    if (VEC) {
-      const float4 v = *reinterpret_cast<const float4*>(y + base + 4 * k);
-      s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
-      ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
-    } else {
-      const double v = y[base + k];
-      s += v;
-      ss += v * v;
+  // two units per thread and trip (both loads in flight first), summed in the one-unit order
+  for (uint32_t e0 = threadIdx.x; e0 < nu; e0 += 512) {
+    float4 vv[2];
+    bool live[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t e = e0 + 256u * h;
+      live[h] = e < nu;
+      vv[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!live[h]) continue;
+      const uint32_t im = fdiv(e, fdu), k = e - im * U;
+      const long base = ((long)(i0 + im) * C + c) * HW;
+      if (VEC)
+        vv[h] = *reinterpret_cast<const float4*>(y + base + 4 * k);
+      else
+        vv[h].x = y[base + k];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!live[h]) continue;
+      const float4 v = vv[h];
+      if (VEC) {
+        s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+        ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+      } else {
+        const double d = v.x;
+        s += d;
+        ss += d * d;
+      }
     }
   }
   s = wave_sum_d(s);
@@ -196,8 +214,9 @@ __device__ __forceinline__ void bn_finalise_plane(const BNStatsIn& s, int c, dou
   const double var = fmax(aa / total - mu * mu, 0.0);
   const float meanf = (float)mu;
   const float isf = (float)(1.0 / sqrt(var + (double)s.eps));
-  sc = s.gamma[c] * isf;
-  sh = s.beta[c] - meanf * sc;
+  // explicit roundings: bn_bwd_* re-derive relu(y*sc + sh) > 0 from y with the same operations
+  sc = __fmul_rn(s.gamma[c], isf);
+  sh = __fmaf_rn(-meanf, sc, s.beta[c]);
   if (owner && (threadIdx.x & 63) == 0) {
     s.mean[c] = meanf;
     s.invstd[c] = isf;
@@ -245,7 +264,8 @@ __global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNApplyFused p, flo
   if (VEC) {
     const long i = 4L * u;
     float4 v = *reinterpret_cast<const float4*>(p.y + i);
-    float r[4] = {v.x * sc + sh, v.y * sc + sh, v.z * sc + sh, v.w * sc + sh};
+    float r[4] = {__fmaf_rn(v.x, sc, sh), __fmaf_rn(v.y, sc, sh), __fmaf_rn(v.z, sc, sh),
+                  __fmaf_rn(v.w, sc, sh)};
     if (p.y2) {
       const float4 q = *reinterpret_cast<const float4*>(p.y2 + i);
       r[0] += q.x * sc2 + sh2; r[1] += q.y * sc2 + sh2; r[2] += q.z * sc2 + sh2; r[3] += q.w * sc2 + sh2;
@@ -260,7 +280,7 @@ __global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNApplyFused p, flo
     }
     *reinterpret_cast<float4*>(out + i) = make_float4(r[0], r[1], r[2], r[3]);
   } else {
-    float r = p.y[u] * sc + sh;
+    float r = __fmaf_rn(p.y[u], sc, sh);
     if (p.y2) r += p.y2[u] * sc2 + sh2;
     if (p.res) r += p.res[u];
     if (p.relu) r = fmaxf(r, 0.f);
@@ -285,41 +305,88 @@ int bn_apply_fused(const BNApplyFused& p, float* out, int N, int C, long HW, hip
   return MD2_OK;
 }
 
+// ReLU mask of a BN+ReLU output without a residual, re-derived from the pre-BN y: the forward's
+// relu(fma(y, sc, sh)) with sc = gamma*invstd, sh = beta - mean*sc in the same explicit roundings
+// (bn_finalise_plane), so the mask is bit-identical and the activation is not read back
+struct YMask {
+  float sc, sh;
+  bool on;
+};
+__device__ __forceinline__ YMask ymask(const float* mgamma, const float* mbeta, int c, float mu, float is) {
+  YMask m{0.f, 0.f, mbeta != nullptr};
+  if (m.on) {
+    m.sc = __fmul_rn(mgamma[c], is);
+    m.sh = __fmaf_rn(-mu, m.sc, mbeta[c]);
+  }
+  return m;
+}
+__device__ __forceinline__ float ymasked(float g, float y, const YMask& m) {
+  return (m.on && !(__fmaf_rn(y, m.sc, m.sh) > 0.f)) ? 0.f : g;
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
-    const float* __restrict__ mean, const float* __restrict__ invstd, int C, int HW, int N,
-    int parts, FastDiv fdu, double* __restrict__ part) {
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ mgamma,
+    const float* __restrict__ mbeta, int C, int HW, int N, int parts, FastDiv fdu,
+    double* __restrict__ part) {
   __shared__ double red[8];
   const int c = blockIdx.x, p = blockIdx.y;
   const int i0 = (int)((long)N * p / parts), i1 = (int)((long)N * (p + 1) / parts);
   const int U = VEC ? HW / 4 : HW;
   const uint32_t nu = (uint32_t)(i1 - i0) * U;
   const float mu = mean[c], is = invstd[c];
+  const YMask ym = ymask(mgamma, mbeta, c, mu, is);
   double sg = 0.0, sgx = 0.0;
-  for (uint32_t e = threadIdx.x; e < nu; e += 256) {
-    const uint32_t im = fdiv(e, fdu), k = e - im * U;
-    const long base = ((long)(i0 + im) * C + c) * HW;
-    if (VEC) {
-      const long i = base + 4 * k;
-      float4 g = *reinterpret_cast<const float4*>(dout + i);
-      if (mask) {
-        const float4 m = *reinterpret_cast<const float4*>(mask + i);
-        if (!(m.x > 0.f)) g.x = 0.f;
-        if (!(m.y > 0.f)) g.y = 0.f;
-        if (!(m.z > 0.f)) g.z = 0.f;
-        if (!(m.w > 0.f)) g.w = 0.f;
+  // two units per thread and trip (both loads in flight before either is used); the sums take
+  // them in the same order as one unit per trip
+  for (uint32_t e0 = threadIdx.x; e0 < nu; e0 += 512) {
+    float4 gv[2], yv[2];
+    bool live[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t e = e0 + 256u * h;
+      live[h] = e < nu;
+      gv[h] = yv[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!live[h]) continue;
+      const uint32_t im = fdiv(e, fdu), k = e - im * U;
+      const long base = ((long)(i0 + im) * C + c) * HW;
+      if (VEC) {
+        const long i = base + 4 * k;
+        gv[h] = *reinterpret_cast<const float4*>(dout + i);
+        yv[h] = *reinterpret_cast<const float4*>(y + i);
+        if (mask) {
+          const float4 m = *reinterpret_cast<const float4*>(mask + i);
+          if (!(m.x > 0.f)) gv[h].x = 0.f;
+          if (!(m.y > 0.f)) gv[h].y = 0.f;
+          if (!(m.z > 0.f)) gv[h].z = 0.f;
+          if (!(m.w > 0.f)) gv[h].w = 0.f;
+        }
+      } else {
+        const long i = base + k;
+        gv[h].x = dout[i];
+        yv[h].x = y[i];
+        if (mask && !(mask[i] > 0.f)) gv[h].x = 0.f;
       }
-      const float4 v = *reinterpret_cast<const float4*>(y + i);
-      sg += (double)g.x + (double)g.y + (double)g.z + (double)g.w;
-      sgx += (double)g.x * (double)((v.x - mu) * is) + (double)g.y * (double)((v.y - mu) * is) +
-             (double)g.z * (double)((v.z - mu) * is) + (double)g.w * (double)((v.w - mu) * is);
-    } else {
-      const long i = base + k;
-      float g = dout[i];
-      if (mask && !(mask[i] > 0.f)) g = 0.f;
-      sg += g;
-      sgx += (double)g * (double)((y[i] - mu) * is);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!live[h]) continue;
+      float4 g = gv[h];
+      const float4 v = yv[h];
+      if (VEC) {
+        g.x = ymasked(g.x, v.x, ym);
+        g.y = ymasked(g.y, v.y, ym);
+        g.z = ymasked(g.z, v.z, ym);
+        g.w = ymasked(g.w, v.w, ym);
+        sg += (double)g.x + (double)g.y + (double)g.z + (double)g.w;
+        sgx += (double)g.x * (double)((v.x - mu) * is) + (double)g.y * (double)((v.y - mu) * is) +
+               (double)g.z * (double)((v.z - mu) * is) + (double)g.w * (double)((v.w - mu) * is);
+      } else {
+        g.x = ymasked(g.x, v.x, ym);
+        sg += g.x;
+        sgx += (double)g.x * (double)((v.x - mu) * is);
+      }
     }
   }
   sg = wave_sum_d(sg);
@@ -350,17 +417,20 @@ __global__ void bn_bwd_final_kernel(const double* __restrict__ part, int C, int 
 }
 
 int bn_bwd_partial(const float* dout, const float* mask_out, const float* y, const float* mean,
-                   const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st) {
+                   const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st,
+                   const float* mgamma, const float* mbeta) {
   MD2_TRY(check_u31((long)N * C * HW));
   MD2_CHECK_ARG(ws.parts >= 1 && ws.parts <= N, "bn_bwd: parts must split the images");
   const int vec = HW % 4 == 0;
   const FastDiv fdu = fd(vec ? HW / 4 : HW);
   if (vec)
     hipLaunchKernelGGL(bn_bwd_partial_kernel<true>, dim3(C, ws.parts), dim3(256), 0, st, dout,
-                       mask_out, y, mean, invstd, C, (int)HW, N, ws.parts, fdu, ws.partials);
+                       mask_out, y, mean, invstd, mgamma, mbeta, C, (int)HW, N, ws.parts, fdu,
+                       ws.partials);
   else
     hipLaunchKernelGGL(bn_bwd_partial_kernel<false>, dim3(C, ws.parts), dim3(256), 0, st, dout,
-                       mask_out, y, mean, invstd, C, (int)HW, N, ws.parts, fdu, ws.partials);
+                       mask_out, y, mean, invstd, mgamma, mbeta, C, (int)HW, N, ws.parts, fdu,
+                       ws.partials);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -374,10 +444,12 @@ int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, cons
   const FastDiv fdu = fd(vec ? HW / 4 : HW);
   if (vec)
     hipLaunchKernelGGL(bn_bwd_partial_kernel<true>, dim3(C, ws.parts), dim3(256), 0, st, dout,
-                       mask_out, y, mean, invstd, C, (int)HW, N, ws.parts, fdu, ws.partials);
+                       mask_out, y, mean, invstd, (const float*)nullptr, (const float*)nullptr, C, (int)HW, N, ws.parts, fdu,
+                       ws.partials);
   else
     hipLaunchKernelGGL(bn_bwd_partial_kernel<false>, dim3(C, ws.parts), dim3(256), 0, st, dout,
-                       mask_out, y, mean, invstd, C, (int)HW, N, ws.parts, fdu, ws.partials);
+                       mask_out, y, mean, invstd, (const float*)nullptr, (const float*)nullptr, C, (int)HW, N, ws.parts, fdu,
+                       ws.partials);
   MD2_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 64)), dim3(64), 0, st, ws.partials, C,
                      ws.parts, dgamma, dbeta);
@@ -468,8 +540,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const double* __restrict__ part, int parts,
     float* __restrict__ dgamma, float* __restrict__ dbeta, uint32_t nu, FastDiv fdU, FastDiv fdC,
-    float invL, float* __restrict__ dy, float* __restrict__ dres, int dres_acc) {
-  __shared__ float s_k0[256], s_db[256], s_dg[256], s_mu[256], s_is[256];
+    float invL, float* __restrict__ dy, float* __restrict__ dres, int dres_acc,
+    const float* __restrict__ mbeta) {
+  __shared__ float s_k0[256], s_db[256], s_dg[256], s_mu[256], s_is[256], s_msc[256], s_msh[256];
   const uint32_t u0 = blockIdx.x * 256u;
   const uint32_t pl0 = fdiv(u0, fdU);
   const uint32_t npl = fdiv(min(u0 + 255u, nu - 1u), fdU) - pl0 + 1u;
@@ -496,6 +569,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
       s_dg[t] = dgf * invL;
       s_mu[t] = mean[c];
       s_is[t] = is;
+      const YMask ym = ymask(gamma, mbeta, c, mean[c], is);
+      s_msc[t] = ym.sc;
+      s_msh[t] = ym.sh;
     }
   }
   __syncthreads();
@@ -503,6 +579,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
   if (u >= nu) return;
   const uint32_t li = fdiv(u, fdU) - pl0;
   const float k0 = s_k0[li], db = s_db[li], dg = s_dg[li], mu = s_mu[li], is = s_is[li];
+  const YMask ym{s_msc[li], s_msh[li], mbeta != nullptr};
   if (VEC) {
     const long i = 4L * u;
     float g[4];
@@ -519,6 +596,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
     }
     const float4 v = *reinterpret_cast<const float4*>(y + i);
     const float yv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[k] = ymasked(g[k], yv[k], ym);
     float r[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) r[k] = k0 * (g[k] - db - (yv[k] - mu) * is * dg);
@@ -534,6 +613,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
   } else {
     float g = dout[u];
     if (mask && !(mask[u] > 0.f)) g = 0.f;
+    g = ymasked(g, y[u], ym);
     const float xh = (y[u] - mu) * is;
     dy[u] = k0 * (g - db - xh * dg);
     if (dres) {
@@ -548,7 +628,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
 int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y, const float* mean,
                        const float* invstd, const float* gamma, BNStatsWs ws, float* dgamma,
                        float* dbeta, int N, int C, long HW, float* dy, float* dres,
-                       int dres_accumulate, hipStream_t st) {
+                       int dres_accumulate, hipStream_t st, const float* mbeta) {
   const long n = (long)N * C * HW;
   MD2_TRY(check_u31(n));
   MD2_CHECK_ARG(ws.partials && ws.parts >= 1, "bn_bwd_apply_fused: missing partials");
@@ -556,11 +636,11 @@ int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y,
   if (HW % 4 == 0)
     hipLaunchKernelGGL(bn_bwd_apply_fused_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st,
                        dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
-                       (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy, dres, dres_accumulate);
+                       (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy, dres, dres_accumulate, mbeta);
   else
     hipLaunchKernelGGL(bn_bwd_apply_fused_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st,
                        dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
-                       (uint32_t)n, fd(HW), fd(C), invL, dy, dres, dres_accumulate);
+                       (uint32_t)n, fd(HW), fd(C), invL, dy, dres, dres_accumulate, mbeta);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
