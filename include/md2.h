@@ -295,6 +295,17 @@ int md2_model_destroy(md2_model* m);
 size_t md2_model_device_bytes(md2_model* m);
 /* re-pack conv weights after the caller changed `params` directly */
 int md2_model_repack(md2_model* m, void* stream);
+/* Flux-layout flat vectors (the order of md2_arch_param_info; conv weights as Flux stores them:
+ * (kw,kh,cin,cout) TRUE-convolution kernels = C-order [cout][cin][kh][kw] with both spatial axes
+ * reversed w.r.t. the library's cross-correlation).  set: copies into the model's params (taps
+ * flipped) and re-packs; get: params -> Flux layout; get_grads: the flat gradient -> Flux layout
+ * (what Zygote returns for Flux.params).  `flux` must not alias the model's vectors. */
+int md2_model_set_params(md2_model* m, const float* flux, void* stream);
+int md2_model_get_params(md2_model* m, float* flux, void* stream);
+int md2_model_get_grads(md2_model* m, float* flux, void* stream);
+/* train_loss pullback with an upstream cotangent (ChainRulesCore rrule): after
+ * md2_model_forward_loss and before backward segment 0, scale the loss-tail gradients by dloss */
+int md2_model_loss_cotangent(md2_model* m, float dloss, void* stream);
 /* forward (encoder on 3*batch frames, decoder on targets, poses) + train_loss value + the
  * loss-tail pullback; terms: [n_levels][2] or NULL.  With cfg.automasking, auto_loss [batch][h][w]
  * is the caller's automasking_loss, or NULL: the library computes it from x (md2_automasking_loss). */

@@ -201,19 +201,37 @@ function gradient!(m::HIPModel; bucket=(off, len) -> nothing)
     return m.∇θ
 end
 
-# Zygote: d(train_loss(...)[1])/dθ.  The library's pullback is for dloss = 1; the scalar
-# cotangent scales it (the loss is a scalar, so that is the exact pullback).
+# Zygote: d(train_loss(...)[1])/dθ.  The loss cotangent enters the library's backward itself
+# (md2_model_loss_cotangent scales the fused loss tail's d disp / d pose before segment 0); the
+# returned tangent is in Flux layout (md2_model_get_grads: conv kernels as true convolutions).
 function ChainRulesCore.rrule(::typeof(train_loss), m::HIPModel, x, auto_loss, cache, params,
                               do_visualization::Bool=false)
     y = train_loss(m, x, auto_loss, cache, params, do_visualization)
     function train_loss_pullback(Δ)
         Δl = Δ[1] isa AbstractZero ? 0f0 : Float32(sum(Array(unthunk(Δ[1]))))
-        ∇ = gradient!(m)
-        Δl == 1f0 || (∇ .*= Δl)
-        return (NoTangent(), Tangent{HIPModel}(; θ=∇), NoTangent(), NoTangent(), NoTangent(),
+        check(ccall((:md2_model_loss_cotangent, lib), Cint, (Ptr{Cvoid}, Cfloat, Ptr{Cvoid}),
+                    m.handle, Δl, stream_ptr()))
+        gradient!(m)
+        ∇flux = similar(m.∇θ)
+        check(ccall((:md2_model_get_grads, lib), Cint, (Ptr{Cvoid}, Ptr{Float32}, Ptr{Cvoid}),
+                    m.handle, ∇flux, stream_ptr()))
+        return (NoTangent(), Tangent{HIPModel}(; θ=∇flux), NoTangent(), NoTangent(), NoTangent(),
                 NoTangent(), NoTangent())
     end
     return y, train_loss_pullback
+end
+
+# Flux-layout parameters in / out of the model (device copies with the conv taps flipped)
+function set_params!(m::HIPModel, flux::ROCVector{Float32})
+    check(ccall((:md2_model_set_params, lib), Cint, (Ptr{Cvoid}, Ptr{Float32}, Ptr{Cvoid}),
+                m.handle, flux, stream_ptr()))
+    return m
+end
+function get_params(m::HIPModel)
+    flux = similar(m.θ)
+    check(ccall((:md2_model_get_params, lib), Cint, (Ptr{Cvoid}, Ptr{Float32}, Ptr{Cvoid}),
+                m.handle, flux, stream_ptr()))
+    return flux
 end
 
 # update!(ADAM(η), θ, ∇θ) -- Flux ADAM, β = (0.9, 0.999), ε = 1e-8 (scripts/script.jl:85)

@@ -424,6 +424,23 @@ int md2_model_train_step_graph(md2_model* m, const float* x, const float* auto_l
                                 (hipStream_t)stream);
 }
 
+int md2_model_set_params(md2_model* m, const float* flux, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_set_params_flux(m->impl, flux, (hipStream_t)stream);
+}
+int md2_model_get_params(md2_model* m, float* flux, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_get_params_flux(m->impl, flux, (hipStream_t)stream);
+}
+int md2_model_get_grads(md2_model* m, float* flux, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_get_grads_flux(m->impl, flux, (hipStream_t)stream);
+}
+int md2_model_loss_cotangent(md2_model* m, float dloss, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_scale_loss_cotangent(m->impl, dloss, (hipStream_t)stream);
+}
+
 int md2_model_set_profiling(md2_model* m, int on) {
   MD2_CHECK_ARG(m, "model");
   return model_set_profiling(m->impl, on);

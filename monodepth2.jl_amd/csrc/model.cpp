@@ -1294,6 +1294,44 @@ int model_profile_read(Model* m, double* out, int ncat) {
   return m->profile_read(out, ncat);
 }
 
+// Flux-layout flat vectors (src/model.jl @functor order, conv weights as true convolutions) <->
+// the library's flat vectors: a copy with every conv weight's taps reversed (md2_model_*_params)
+static int flux_flip_copy(const Model* m, const float* src, float* dst, hipStream_t st) {
+  MD2_CHECK_ARG(src && dst && src != dst, "params: distinct source and destination required");
+  MD2_HIP(hipMemcpyAsync(dst, src, sizeof(float) * (size_t)m->spec.total, hipMemcpyDeviceToDevice, st));
+  for (const ParamEntry& e : m->spec.table)
+    if (e.ndim == 4 && e.shape[2] * e.shape[3] > 1)
+      MD2_TRY(flip_taps(src + e.offset, dst + e.offset, (long)e.shape[0] * e.shape[1], e.shape[2],
+                        e.shape[3], st));
+  return MD2_OK;
+}
+
+int model_set_params_flux(Model* m, const float* flux, hipStream_t st) {
+  MD2_CHECK_ARG(m, "model");
+  MD2_TRY(flux_flip_copy(m, flux, m->params, st));
+  return m->repack(st);
+}
+
+int model_get_params_flux(Model* m, float* flux, hipStream_t st) {
+  MD2_CHECK_ARG(m, "model");
+  return flux_flip_copy(m, m->params, flux, st);
+}
+
+int model_get_grads_flux(Model* m, float* flux, hipStream_t st) {
+  MD2_CHECK_ARG(m, "model");
+  return flux_flip_copy(m, m->grads, flux, st);
+}
+
+// train_loss pullback with an upstream cotangent: the fused loss tail formed d loss / d (disp,
+// pose) for dloss = 1 during the forward; scale them before backward segment 0
+int model_scale_loss_cotangent(Model* m, float dloss, hipStream_t st) {
+  MD2_CHECK_ARG(m && m->cur_x, "loss cotangent before forward");
+  if (dloss == 1.f) return MD2_OK;
+  for (auto& d : m->br)
+    if (d.head >= 0) MD2_TRY(scale_inplace(d.d_head, (long)m->N * 4 * d.h * d.w, dloss, st));
+  return scale_inplace(m->d_pose, 2L * m->N * 6, dloss, st);
+}
+
 long model_param_count(Model* m) { return m ? m->spec.total : 0; }
 float* model_grads(Model* m) { return m ? m->grads : nullptr; }
 size_t model_device_bytes(Model* m) { return m ? m->bytes : 0; }

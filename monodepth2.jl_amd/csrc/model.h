@@ -75,6 +75,12 @@ int model_features(Model* m, const float** feat, int* c, int* h, int* w);
 int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipStream_t st);
 int model_debug_tensor(Model* m, int index, const char** name, const void** ptr, int* dims);
 long model_param_count(Model* m);
+// flat vectors in Flux layout (conv weights as true convolutions: taps reversed)
+int model_set_params_flux(Model* m, const float* flux, hipStream_t st);
+int model_get_params_flux(Model* m, float* flux, hipStream_t st);
+int model_get_grads_flux(Model* m, float* flux, hipStream_t st);
+// scale the loss-tail gradients of the last forward by the train_loss cotangent
+int model_scale_loss_cotangent(Model* m, float dloss, hipStream_t st);
 float* model_grads(Model* m);          // the caller-owned flat gradient vector
 size_t model_device_bytes(Model* m);
 

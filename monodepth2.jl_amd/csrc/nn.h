@@ -97,6 +97,9 @@ int pair_grad_gather(const float* dpin, int N, int C, long HW, const int a[2], c
                      float* dsq, hipStream_t st);
 
 // ---- Flux ADAM over the flat parameter vector ----
+int scale_inplace(float* x, long n, float s, hipStream_t st);
+// [planes][kh][kw] with both spatial axes reversed (Flux true-convolution <-> cross-correlation)
+int flip_taps(const float* src, float* dst, long planes, int kh, int kw, hipStream_t st);
 // graph-replayable ADAM: *step += 1 and bc = (1 - b1^t, 1 - b2^t) on the device, then the update
 int adam_prep(int* step, float* bc, float b1, float b2, hipStream_t st);
 int set_device_int(int* p, int v, hipStream_t st);

@@ -1178,6 +1178,37 @@ int adam_step_dev(float* p, const float* g, float* m, float* v, long n, float lr
   return MD2_OK;
 }
 
+// x *= s (train_loss pullback cotangent on the loss-tail gradients)
+__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ x, long n, float s) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] *= s;
+}
+int scale_inplace(float* x, long n, float s, hipStream_t st) {
+  if (n <= 0) return MD2_OK;
+  hipLaunchKernelGGL(scale_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, x, n, s);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// Flux Conv weights (kw,kh,cin,cout) = C-order [cout][cin][kh][kw] of a TRUE convolution ->
+// the library's cross-correlation layout (and back: the map is an involution): both spatial axes
+// reversed, dst[o][i][y][x] = src[o][i][kh-1-y][kw-1-x]
+__global__ __launch_bounds__(256) void flip_taps_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                        long planes, int kh, int kw) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long kk = (long)kh * kw;
+  if (i >= planes * kk) return;
+  const long pl = i / kk;
+  const int t = (int)(i - pl * kk), y = t / kw, x = t - y * kw;
+  dst[i] = src[pl * kk + (long)(kh - 1 - y) * kw + (kw - 1 - x)];
+}
+int flip_taps(const float* src, float* dst, long planes, int kh, int kw, hipStream_t st) {
+  hipLaunchKernelGGL(flip_taps_kernel, dim3(cdiv(planes * kh * kw, 256)), dim3(256), 0, st, src, dst,
+                     planes, kh, kw);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 int adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
               float eps, float bc1, float bc2, float gscale, hipStream_t st) {
   hipLaunchKernelGGL(adam_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, p, g, m, v, n, lr, b1, b2,

@@ -108,6 +108,10 @@ _SIGS = {
     "md2_model_adam": (C.c_int, [P, P, P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_float, P]),
     "md2_model_train_step": (C.c_int, [P, P, P, P, P, C.c_float, C.c_int, P, P]),
     "md2_model_train_step_graph": (C.c_int, [P, P, P, P, P, C.c_float, C.c_int, P, P]),
+    "md2_model_set_params": (C.c_int, [P, P, P]),
+    "md2_model_get_params": (C.c_int, [P, P, P]),
+    "md2_model_get_grads": (C.c_int, [P, P, P]),
+    "md2_model_loss_cotangent": (C.c_int, [P, C.c_float, P]),
     "md2_model_outputs": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.POINTER(C.c_void_p)]),
     "md2_model_eval_disparity": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_void_p), P]),

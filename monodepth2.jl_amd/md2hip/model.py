@@ -391,13 +391,42 @@ def train_loss(model: Model, x, auto_loss, cache: TrainCache, params: Params,
             vis["vis_loss"][-1].unsqueeze(1).cpu())
 
 
-def gradient(model: Model):
-    """Backward of the last ``train_loss`` (Zygote ``gradient(θ)``): fills ``model.grad``."""
+def gradient(model: Model, dloss: float = 1.0):
+    """Backward of the last ``train_loss`` (Zygote ``gradient(θ)``): fills ``model.grad``.
+    ``dloss`` is the upstream cotangent of the loss (the ``rrule`` pullback's input)."""
     ex = model._last
     if not ex.forwarded:
         raise RuntimeError("gradient() needs a preceding train_loss()")
+    if dloss != 1.0:
+        check(lib().md2_model_loss_cotangent(ex.handle, float(dloss), stream_of(model.device)),
+              "md2_model_loss_cotangent")
     ex.backward()
     return model.grad
+
+
+def set_flux_params(model: Model, flux_flat):
+    """Load a Flux-layout flat vector (``Flux.params`` order, conv kernels as true convolutions)
+    into the model: taps flipped on the device (md2_model_set_params), every executor re-packs."""
+    import torch
+    src = flux_flat.to(device=model.device, dtype=torch.float32).contiguous()
+    ex = model._last or next(iter(model._ex.values()), None)
+    if ex is None:
+        raise RuntimeError("set_flux_params needs an executor (run train_loss / eval_disparity once)")
+    check(lib().md2_model_set_params(ex.handle, ptr(src), stream_of(model.device)), "md2_model_set_params")
+    model.touch()
+    ex.version = model.version
+
+
+def flux_params(model: Model, grads: bool = False):
+    """The flat parameters (or gradients) in Flux layout (md2_model_get_params / _get_grads)."""
+    import torch
+    ex = model._last or next(iter(model._ex.values()), None)
+    if ex is None:
+        raise RuntimeError("flux_params needs an executor")
+    out = torch.empty_like(model.flat)
+    fn = lib().md2_model_get_grads if grads else lib().md2_model_get_params
+    check(fn(ex.handle, ptr(out), stream_of(model.device)), "md2_model_get_params")
+    return out
 
 
 class ADAM:

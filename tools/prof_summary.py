@@ -35,6 +35,8 @@ def is_conv3(name):
         return a[5] == 3 and a[8] == 0
     if "conv_px_kernel" in name:          # <MODE, TAP, BM, BN, BK, WM, WN, KH, KW, S, RFL>
         return a[7] == 3 and a[10] == 0
+    if "conv_wgrad_stem_kernel" in name:   # <CIN>: the 7x7/2 stem
+        return False
     if "conv_wgrad16_kernel" in name:      # <MT, KH, KW, RFL>
         return a[1] == 3 and a[3] == 0
     if "conv_wgrad" in name:               # <BM, BN, BK, WM, WN, KH, KW, S, RFL[, CW]>
