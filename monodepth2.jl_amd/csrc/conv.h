@@ -41,6 +41,17 @@ struct TensorOut {
   int accumulate = 0;      // out += result
 };
 
+// Launch-boundary split-K reduce: with a SplitKDefer, a fwd/dgrad launch that runs split-K into
+// a plain output (stride 1, no bias/activation/accumulate/concat, contiguous images) does NOT
+// launch its reduction; `slab`/`splits` describe the [splits][M][N] partial slabs in the conv
+// workspace and the caller's next kernel sums them (bn_stats_partial_slabs /
+// bn_bwd_partial_slabs) before any other conv reuses the workspace.  splits == 0: the output was
+// written as usual.
+struct SplitKDefer {
+  const float* slab = nullptr;
+  int splits = 0;
+};
+
 struct ConvWorkspace {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -89,10 +100,10 @@ size_t conv_dgrad_workspace(const ConvShape& s);
 size_t conv_wgrad_workspace(const ConvShape& s);
 
 int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const TensorOut& y,
-             ConvWorkspace ws, hipStream_t st);
+             ConvWorkspace ws, hipStream_t st, SplitKDefer* defer = nullptr);
 // dX from dY (dY: [N][Cout][Ho][Wo] pre-activation gradient)
 int conv_dgrad(const ConvShape& s, const float* dy, const float* wpacked_d, const TensorOut& dx,
-               ConvWorkspace ws, hipStream_t st);
+               ConvWorkspace ws, hipStream_t st, SplitKDefer* defer = nullptr);
 // dW [Cout][Cin*KH*KW] (store or accumulate) and optional db [Cout]
 // db_part/db_parts: bias-gradient partials [Cout][db_parts] already summed by act_backward_bias
 // (the bias partial pass over dY is then skipped)

@@ -596,6 +596,34 @@ class Model {
     prof_end(e, c.cat, conv_flops(s), st, "fwd", &s);
     return MD2_OK;
   }
+  // conv + BatchNorm statistics: a split-K conv leaves its slabs to the statistics pass, which
+  // sums them (bit-identical to the conv's own reduction), writes y and takes the partials in one
+  // launch.  The profile bracket then includes that fused pass (conservative for the roofline).
+  int conv_f_bn(RConv& c, int nimg, const TensorIn& in, float* y, long out_bs, RBN& bn, long HW,
+                hipStream_t st, int slot = 0) {
+    ConvShape s = c.s;
+    s.N = nimg;
+    TensorOut o;
+    o.p0 = y;
+    o.bs0 = out_bs;
+    o.bias = P(c.p.b);
+    SplitKDefer d;
+    hipEvent_t e = prof_begin(st);
+    MD2_TRY(conv_fwd(s, in, c.wpf, o, cws, st, fuse_splitk ? &d : nullptr));
+    if (d.splits > 0) {
+      BNStatsWs w = bn_ws(bn, nimg, HW, slot);
+      MD2_TRY(bn_stats_partial_slabs(SlabIn{d.slab, d.splits}, y, nimg, bn.p.c, HW, w, st));
+      prof_end(e, c.cat, conv_flops(s), st, "fwd", &s);
+      return MD2_OK;
+    }
+    prof_end(e, c.cat, conv_flops(s), st, "fwd", &s);
+    return bn_fwd(bn, y, nimg, HW, st, slot);
+  }
+  // MD2_FUSE_SPLITK=0 restores the separate reduction launches (A/B measurement)
+  const bool fuse_splitk = [] {
+    const char* v = getenv("MD2_FUSE_SPLITK");
+    return !(v && v[0] == '0');
+  }();
   static TensorIn tin(const float* p, int C, long HW) {
     TensorIn t;
     t.p0 = p;
@@ -645,13 +673,16 @@ class Model {
   int repack(hipStream_t st) { return conv_pack_batch(pack_jobs, pack_njobs, pack_blocks, st); }
 
   // statistics partials only; the finalise is fused into the apply (bn_apply_fused)
-  int bn_fwd(RBN& bn, const float* y, int nimg, long HW, hipStream_t st, int slot = 0) {
+  BNStatsWs bn_ws(RBN& bn, int nimg, long HW, int slot) {
     BNStatsWs w = bnws;
     w.partials += slot * bn_slot;
     w.parts = bn_parts(bn.p.c, nimg, HW);
     bn.part = w.partials;
     bn.parts = w.parts;
-    return bn_stats_partial(y, nimg, bn.p.c, HW, w, st);
+    return w;
+  }
+  int bn_fwd(RBN& bn, const float* y, int nimg, long HW, hipStream_t st, int slot = 0) {
+    return bn_stats_partial(y, nimg, bn.p.c, HW, bn_ws(bn, nimg, HW, slot), st);
   }
   BNStatsIn bn_in(const RBN& bn) {
     BNStatsIn s;
@@ -669,8 +700,7 @@ class Model {
   // ---- encoder forward over nimg images (input already mapped by `in`)
   int encoder_fwd(const TensorIn& in, int nimg, hipStream_t st) {
     const long hw0 = (long)H0 * W0;
-    MD2_TRY(conv_f(stem, nimg, in, y0, 64 * hw0, ACT_NONE, 0, st));
-    MD2_TRY(bn_fwd(stem_bn, y0, nimg, hw0, st));
+    MD2_TRY(conv_f_bn(stem, nimg, in, y0, 64 * hw0, stem_bn, hw0, st));
     BNApplyFused ap{};
     ap.y = y0; ap.s1 = bn_in(stem_bn); ap.relu = 1;
     MD2_TRY(bn_apply_fused(ap, f0, nimg, 64, hw0, st));
@@ -683,8 +713,7 @@ class Model {
         for (size_t k = 0; k < b.st.size(); ++k) {
           EncStage& e = b.st[k];
           const long ohw = (long)e.conv.s.Ho * e.conv.s.Wo;
-          MD2_TRY(conv_f(e.conv, nimg, tin(x, C, HW), e.y, (long)e.conv.p.cout * ohw, ACT_NONE, 0, st));
-          MD2_TRY(bn_fwd(e.bn, e.y, nimg, ohw, st));
+          MD2_TRY(conv_f_bn(e.conv, nimg, tin(x, C, HW), e.y, (long)e.conv.p.cout * ohw, e.bn, ohw, st));
           if (k + 1 < b.st.size()) {
             BNApplyFused a{};
             a.y = e.y; a.s1 = bn_in(e.bn); a.relu = 1;
@@ -699,8 +728,7 @@ class Model {
         BNApplyFused a{};
         a.y = last.y; a.s1 = bn_in(last.bn); a.relu = 1;
         if (b.down) {
-          MD2_TRY(conv_f(b.dconv, nimg, tin(b.in, b.Cin, (long)b.Hin * b.Win), b.yd, (long)b.C * ohw, ACT_NONE, 0, st));
-          MD2_TRY(bn_fwd(b.dbn, b.yd, nimg, ohw, st, 1));
+          MD2_TRY(conv_f_bn(b.dconv, nimg, tin(b.in, b.Cin, (long)b.Hin * b.Win), b.yd, (long)b.C * ohw, b.dbn, ohw, st, 1));
           a.y2 = b.yd; a.s2 = bn_in(b.dbn);
         } else {
           a.res = b.in;
@@ -873,6 +901,31 @@ class Model {
     prof_end(e, c.cat, conv_flops(s), st, "dgrad", &s);
     return MD2_OK;
   }
+  // dgrad into DA followed by the backward of the residual-free BN+ReLU that produced the conv's
+  // input (ReLU mask re-derived from y): a split-K dgrad leaves its slabs to bn_bwd_partial, which
+  // forms DA in the same pass (profile bracket includes it, as conv_f_bn)
+  int conv_d_bn(RConv& c, int nimg, const float* dy, float* da, long da_bs, RBN& bn, const float* y,
+                long HW, float* dyprev, hipStream_t st) {
+    ConvShape s = c.s;
+    s.N = nimg;
+    TensorOut o;
+    o.p0 = da;
+    o.bs0 = da_bs;
+    SplitKDefer d;
+    hipEvent_t e = prof_begin(st);
+    MD2_TRY(conv_dgrad(s, dy, c.wpd, o, cws, st, fuse_splitk ? &d : nullptr));
+    if (d.splits == 0) {
+      prof_end(e, c.cat, conv_flops(s), st, "dgrad", &s);
+      return bn_bwd(bn, da, nullptr, y, nimg, HW, dyprev, nullptr, 0, st, true);
+    }
+    BNStatsWs w = bnws;
+    w.parts = bn_parts(bn.p.c, nimg, HW);
+    MD2_TRY(bn_bwd_partial_slabs(SlabIn{d.slab, d.splits}, da, y, bn.mean, bn.invstd, nimg, bn.p.c,
+                                 HW, w, st, P(bn.p.g), P(bn.p.b)));
+    prof_end(e, c.cat, conv_flops(s), st, "dgrad", &s);
+    return bn_bwd_apply_fused(da, nullptr, y, bn.mean, bn.invstd, P(bn.p.g), w, Gd(bn.p.g),
+                              Gd(bn.p.b), nimg, bn.p.c, HW, dyprev, nullptr, 0, st, P(bn.p.b));
+  }
   // activation pullback fused with the bias-gradient partials of the conv that produced `out`
   // (consumed by that conv's next conv_w)
   float* bp_ws = nullptr;
@@ -922,9 +975,9 @@ class Model {
       const int cin = e.conv.p.cin;
       const long hin = (long)e.conv.s.H * e.conv.s.W;
       if (k > 0) {
-        MD2_TRY(conv_wd(e.conv, nimg, tin(xin, cin, hin), DY, DA, (long)cin * hin, 0, st));
+        MD2_TRY(conv_w(e.conv, nimg, tin(xin, cin, hin), DY, st));
         EncStage& pe = b.st[k - 1];
-        MD2_TRY(bn_bwd(pe.bn, DA, pe.a, pe.y, nimg, hin, DY, nullptr, 0, st, true));
+        MD2_TRY(conv_d_bn(e.conv, nimg, DY, DA, (long)cin * hin, pe.bn, pe.y, hin, DY, st));
       } else {
         MD2_TRY(conv_wd(e.conv, nimg, tin(xin, cin, hin), DY, b.d_in, (long)cin * hin, 1, st));
       }

@@ -11,6 +11,14 @@ struct BNStatsWs {
   int parts;
 };
 int bn_parts(int C, long N, long HW);
+// Split-K slabs [splits][C][N*HW] of the conv that produced a BN input (conv_fwd / conv_dgrad
+// with a SplitKDefer): the BN kernels below sum them in split order -- the conv's own reduction,
+// bit-identical -- write the tensor and take its partials in the same pass (the launch-boundary
+// reduce: one launch and one full read of the tensor fewer)
+struct SlabIn {
+  const float* slab = nullptr;
+  int splits = 0;
+};
 // mean/invstd [C]; running stats updated when run_mean != nullptr (momentum, unbiased var)
 int bn_stats(const float* y, int N, int C, long HW, float eps, float momentum, float* mean,
              float* invstd, float* run_mean, float* run_var, BNStatsWs ws, hipStream_t st);
@@ -43,6 +51,7 @@ struct BNApplyFused {
   int relu = 0;
 };
 int bn_stats_partial(const float* y, int N, int C, long HW, BNStatsWs ws, hipStream_t st);
+int bn_stats_partial_slabs(SlabIn sl, float* y, int N, int C, long HW, BNStatsWs ws, hipStream_t st);
 int bn_apply_fused(const BNApplyFused& p, float* out, int N, int C, long HW, hipStream_t st);
 // backward reduce: g = dout * (mask_out > 0 if mask_out) ; dgamma = sum g*xhat, dbeta = sum g
 int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, const float* mean,
@@ -55,6 +64,10 @@ int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, cons
 int bn_bwd_partial(const float* dout, const float* mask_out, const float* y, const float* mean,
                    const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st,
                    const float* mgamma = nullptr, const float* mbeta = nullptr);
+// the same with dout formed from the dgrad's split-K slabs (and written to dout)
+int bn_bwd_partial_slabs(SlabIn sl, float* dout, const float* y, const float* mean,
+                         const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st,
+                         const float* mgamma, const float* mbeta);
 int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y, const float* mean,
                        const float* invstd, const float* gamma, BNStatsWs ws, float* dgamma,
                        float* dbeta, int N, int C, long HW, float* dy, float* dres,

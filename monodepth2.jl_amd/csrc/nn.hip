@@ -23,15 +23,21 @@ static int check_u31(long n) {
 
 // One block per (channel c, image group p): the group's images x HW elements of channel c,
 // walked as a flat range (float4 units when HW % 4 == 0); fp64 accumulation.
-template <bool VEC>
+// SLAB: y is not read but formed here from the split-K slabs of the conv that produced it
+// (sum in split order = the conv's own reduction, bit-identical) and written to yout -- the
+// conv's separate reduction launch and one read of y disappear
+template <bool VEC, bool SLAB = false>
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ y, int C,
                                                                int HW, int N, int parts,
-                                                               FastDiv fdu, double* __restrict__ part) {
+                                                               FastDiv fdu, double* __restrict__ part,
+                                                               SlabIn sl = SlabIn{},
+                                                               float* __restrict__ yout = nullptr) {
   __shared__ double red[8];
   const int c = blockIdx.x, p = blockIdx.y;
   const int i0 = (int)((long)N * p / parts), i1 = (int)((long)N * (p + 1) / parts);
   const int U = VEC ? HW / 4 : HW;                 // units per image
   const uint32_t nu = (uint32_t)(i1 - i0) * U;
+  const long sstride = (long)C * N * HW;           // one slab [C][N*HW]
   double s = 0.0, ss = 0.0;
   // two units per thread and trip (both loads in flight first), summed in the one-unit order
   for (uint32_t e0 = threadIdx.x; e0 < nu; e0 += 512) {
@@ -45,10 +51,23 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
       if (!live[h]) continue;
       const uint32_t im = fdiv(e, fdu), k = e - im * U;
       const long base = ((long)(i0 + im) * C + c) * HW;
-      if (VEC)
+      if (SLAB) {
+        const long si = (long)c * N * HW + (long)(i0 + im) * HW + (VEC ? 4 * k : k);
+        if (VEC) {
+          for (int q = 0; q < sl.splits; ++q) {
+            const float4 t = *reinterpret_cast<const float4*>(sl.slab + q * sstride + si);
+            vv[h].x += t.x; vv[h].y += t.y; vv[h].z += t.z; vv[h].w += t.w;
+          }
+          *reinterpret_cast<float4*>(yout + base + 4 * k) = vv[h];
+        } else {
+          for (int q = 0; q < sl.splits; ++q) vv[h].x += sl.slab[q * sstride + si];
+          yout[base + k] = vv[h].x;
+        }
+      } else if (VEC) {
         vv[h] = *reinterpret_cast<const float4*>(y + base + 4 * k);
-      else
+      } else {
         vv[h].x = y[base + k];
+      }
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -110,6 +129,22 @@ int bn_stats_partial(const float* y, int N, int C, long HW, BNStatsWs ws, hipStr
   else
     hipLaunchKernelGGL(bn_stats_partial_kernel<false>, dim3(C, ws.parts), dim3(256), 0, st, y, C,
                        (int)HW, N, ws.parts, fdu, ws.partials);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int bn_stats_partial_slabs(SlabIn sl, float* y, int N, int C, long HW, BNStatsWs ws, hipStream_t st) {
+  MD2_TRY(check_u31((long)N * C * HW));
+  MD2_CHECK_ARG(ws.parts >= 1 && ws.parts <= N, "bn_stats: parts must split the images");
+  MD2_CHECK_ARG(sl.slab && sl.splits >= 1 && y, "bn_stats_partial_slabs: slabs / output");
+  const int vec = HW % 4 == 0;
+  const FastDiv fdu = fd(vec ? HW / 4 : HW);
+  if (vec)
+    hipLaunchKernelGGL((bn_stats_partial_kernel<true, true>), dim3(C, ws.parts), dim3(256), 0, st,
+                       (const float*)nullptr, C, (int)HW, N, ws.parts, fdu, ws.partials, sl, y);
+  else
+    hipLaunchKernelGGL((bn_stats_partial_kernel<false, true>), dim3(C, ws.parts), dim3(256), 0, st,
+                       (const float*)nullptr, C, (int)HW, N, ws.parts, fdu, ws.partials, sl, y);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -324,12 +359,13 @@ __device__ __forceinline__ float ymasked(float g, float y, const YMask& m) {
   return (m.on && !(__fmaf_rn(y, m.sc, m.sh) > 0.f)) ? 0.f : g;
 }
 
-template <bool VEC>
+// SLAB: dout formed from the dgrad conv's split-K slabs and written (see bn_stats_partial_kernel)
+template <bool VEC, bool SLAB = false>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ mgamma,
     const float* __restrict__ mbeta, int C, int HW, int N, int parts, FastDiv fdu,
-    double* __restrict__ part) {
+    double* __restrict__ part, SlabIn sl = SlabIn{}, float* __restrict__ dout_w = nullptr) {
   __shared__ double red[8];
   const int c = blockIdx.x, p = blockIdx.y;
   const int i0 = (int)((long)N * p / parts), i1 = (int)((long)N * (p + 1) / parts);
@@ -337,6 +373,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
   const uint32_t nu = (uint32_t)(i1 - i0) * U;
   const float mu = mean[c], is = invstd[c];
   const YMask ym = ymask(mgamma, mbeta, c, mu, is);
+  const long sstride = (long)C * N * HW;
   double sg = 0.0, sgx = 0.0;
   // two units per thread and trip (both loads in flight before either is used); the sums take
   // them in the same order as one unit per trip
@@ -351,9 +388,22 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
       if (!live[h]) continue;
       const uint32_t im = fdiv(e, fdu), k = e - im * U;
       const long base = ((long)(i0 + im) * C + c) * HW;
+      if (SLAB) {
+        const long si = (long)c * N * HW + (long)(i0 + im) * HW + (VEC ? 4 * k : k);
+        if (VEC) {
+          for (int q = 0; q < sl.splits; ++q) {
+            const float4 t = *reinterpret_cast<const float4*>(sl.slab + q * sstride + si);
+            gv[h].x += t.x; gv[h].y += t.y; gv[h].z += t.z; gv[h].w += t.w;
+          }
+          *reinterpret_cast<float4*>(dout_w + base + 4 * k) = gv[h];
+        } else {
+          for (int q = 0; q < sl.splits; ++q) gv[h].x += sl.slab[q * sstride + si];
+          dout_w[base + k] = gv[h].x;
+        }
+      }
       if (VEC) {
         const long i = base + 4 * k;
-        gv[h] = *reinterpret_cast<const float4*>(dout + i);
+        if (!SLAB) gv[h] = *reinterpret_cast<const float4*>(dout + i);
         yv[h] = *reinterpret_cast<const float4*>(y + i);
         if (mask) {
           const float4 m = *reinterpret_cast<const float4*>(mask + i);
@@ -364,7 +414,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
         }
       } else {
         const long i = base + k;
-        gv[h].x = dout[i];
+        if (!SLAB) gv[h].x = dout[i];
         yv[h].x = y[i];
         if (mask && !(mask[i] > 0.f)) gv[h].x = 0.f;
       }
@@ -431,6 +481,26 @@ int bn_bwd_partial(const float* dout, const float* mask_out, const float* y, con
     hipLaunchKernelGGL(bn_bwd_partial_kernel<false>, dim3(C, ws.parts), dim3(256), 0, st, dout,
                        mask_out, y, mean, invstd, mgamma, mbeta, C, (int)HW, N, ws.parts, fdu,
                        ws.partials);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+int bn_bwd_partial_slabs(SlabIn sl, float* dout, const float* y, const float* mean,
+                         const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st,
+                         const float* mgamma, const float* mbeta) {
+  MD2_TRY(check_u31((long)N * C * HW));
+  MD2_CHECK_ARG(ws.parts >= 1 && ws.parts <= N, "bn_bwd: parts must split the images");
+  MD2_CHECK_ARG(sl.slab && sl.splits >= 1 && dout, "bn_bwd_partial_slabs: slabs / output");
+  const int vec = HW % 4 == 0;
+  const FastDiv fdu = fd(vec ? HW / 4 : HW);
+  if (vec)
+    hipLaunchKernelGGL((bn_bwd_partial_kernel<true, true>), dim3(C, ws.parts), dim3(256), 0, st,
+                       (const float*)nullptr, (const float*)nullptr, y, mean, invstd, mgamma, mbeta, C,
+                       (int)HW, N, ws.parts, fdu, ws.partials, sl, dout);
+  else
+    hipLaunchKernelGGL((bn_bwd_partial_kernel<false, true>), dim3(C, ws.parts), dim3(256), 0, st,
+                       (const float*)nullptr, (const float*)nullptr, y, mean, invstd, mgamma, mbeta, C,
+                       (int)HW, N, ws.parts, fdu, ws.partials, sl, dout);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
