@@ -54,6 +54,7 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
       if (SLAB) {
         const long si = (long)c * N * HW + (long)(i0 + im) * HW + (VEC ? 4 * k : k);
         if (VEC) {
+#pragma unroll 4
           for (int q = 0; q < sl.splits; ++q) {
             const float4 t = *reinterpret_cast<const float4*>(sl.slab + q * sstride + si);
             vv[h].x += t.x; vv[h].y += t.y; vv[h].z += t.z; vv[h].w += t.w;
@@ -391,6 +392,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
       if (SLAB) {
         const long si = (long)c * N * HW + (long)(i0 + im) * HW + (VEC ? 4 * k : k);
         if (VEC) {
+#pragma unroll 4
           for (int q = 0; q < sl.splits; ++q) {
             const float4 t = *reinterpret_cast<const float4*>(sl.slab + q * sstride + si);
             gv[h].x += t.x; gv[h].y += t.y; gv[h].z += t.z; gv[h].w += t.w;
