@@ -64,6 +64,10 @@ struct SmoothArgs {
   int N, W, H;
 };
 
+struct SmoothBatch {
+  SmoothArgs s[MAX_SCALES];  // every scale shares N, W, H (full resolution)
+};
+
 struct UpAdjArgs {
   const float* g_full;       // [N][H][W]
   const float* disp;         // [N][dh][dw] sigmoid output (for the derivative)
@@ -78,6 +82,22 @@ struct UpAdjArgs {
   int accumulate;
   float* out;                // [N][dh][dw]
   int N, W, H;
+};
+
+struct UpAdjBatch {
+  UpAdjArgs s[MAX_SCALES];   // every scale shares N and W
+};
+
+// per-image sums of one scale's upsampled disparity (the smoothness mean normalisation)
+struct DispSumArgs {
+  const float* disp;         // [N][dh][dw]
+  int dw, dh;
+  float rx, ry;
+  float* out;                // [N][parts]
+};
+struct DispSumBatch {
+  DispSumArgs s[MAX_SCALES];
+  int W, H, N, parts;
 };
 
 struct FinalizeArgs {
@@ -104,10 +124,10 @@ int launch_warp_vis(const PhotoArgs& a, int scale, const Geom& g, int C, float* 
 // partial rows per scale of the photometric pass run with `nscales` scales
 long photometric_blocks(int W, int H, int N, int nscales);
 long smooth_blocks(int W, int H, int N);
-int launch_disp_sum(const float* disp, int dw, int dh, float rx, float ry, int W, int H, int N,
-                    int parts, float* out, hipStream_t st);
-int launch_smooth(const SmoothArgs& a, int C, hipStream_t st);
-int launch_up_adjoint(const UpAdjArgs& a, hipStream_t st);
+// the next three run every scale of the loss tail in ONE launch each (scale = grid z)
+int launch_disp_sum(const DispSumBatch& b, int nscales, hipStream_t st);
+int launch_smooth(const SmoothArgs* a, int nscales, int C, hipStream_t st);
+int launch_up_adjoint(const UpAdjArgs* a, int nscales, hipStream_t st);
 int launch_loss_finalize(const FinalizeArgs& a, float* dRt, float* loss, hipStream_t st);
 // per-(source, sample) sums of the photometric blocks' pose partials -> dRt [2N][12]
 int launch_pose_grad_reduce(const FinalizeArgs& a, float* dRt, hipStream_t st);

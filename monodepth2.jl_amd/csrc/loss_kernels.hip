@@ -4,6 +4,8 @@
 //
 // Reference: src/training.jl:21-78 (train_loss), src/utils.jl:106-145 (so3 + hat),
 // :163-183 (smooth_loss, disparity_to_depth), :185-192 (composeT).
+#include <algorithm>
+
 #include "loss_kernels.h"
 
 namespace md2 {
@@ -69,21 +71,22 @@ __device__ __forceinline__ void ray_at(const Geom& g, int gx, int gy, float& r0,
 // ---------------------------------------------------------------------------------------------
 // per-image mean of the (upsampled) disparity -- src/training.jl:64-65
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void disp_sum_kernel(const float* __restrict__ disp, int dw,
-                                                       int dh, float rx, float ry, int W, int H,
-                                                       int parts, float* __restrict__ out) {
+// all scales in one launch: grid (parts, N, nscales)
+__global__ __launch_bounds__(256) void disp_sum_kernel(DispSumBatch b) {
   __shared__ float red[4];
   const int n = blockIdx.y;
+  const DispSumArgs a = b.s[blockIdx.z];
+  const int W = b.W, H = b.H, parts = b.parts;
   const long P = (long)W * H;
-  const float* d = disp + (long)n * dw * dh;
+  const float* d = a.disp + (long)n * a.dw * a.dh;
   float s = 0.f;
   for (long q = (long)blockIdx.x * 256 + threadIdx.x; q < P; q += (long)parts * 256) {
     const int X = (int)(q % W), Y = (int)(q / W);
-    s += disp_at(d, dw, dh, rx, ry, W, H, X, Y);
+    s += disp_at(d, a.dw, a.dh, a.rx, a.ry, W, H, X, Y);
   }
   float v[1] = {s};
   block_sum256<1>(v, red);
-  if (threadIdx.x == 0) out[n * parts + blockIdx.x] = v[0];
+  if (threadIdx.x == 0) a.out[n * parts + blockIdx.x] = v[0];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -93,13 +96,15 @@ __global__ __launch_bounds__(256) void disp_sum_kernel(const float* __restrict__
 constexpr int SM_W = 64, SM_H = 4;
 
 template <int C>
-__global__ __launch_bounds__(256) void smooth_kernel(SmoothArgs a) {
+__global__ __launch_bounds__(256) void smooth_kernel(SmoothBatch b) {
   constexpr int EW = SM_W + 1, EH = SM_H + 1, NE = EW * EH;
   __shared__ float s_ex[NE], s_ey[NE];
   __shared__ float s_red[4 * 3];
+  const int sc = blockIdx.z / b.s[0].N;       // scale; every scale shares N, W, H
+  const SmoothArgs a = b.s[sc];
   const int W = a.W, H = a.H;
   const long HW = (long)W * H;
-  const int n = blockIdx.z;
+  const int n = blockIdx.z - sc * a.N;
   const int x0 = blockIdx.x * SM_W, y0 = blockIdx.y * SM_H;
   const float* dsp = a.disp + (long)n * a.dw * a.dh;
   const float* img = a.img + (long)n * a.img_sample_stride;
@@ -195,11 +200,14 @@ __device__ __forceinline__ float up_weight(int X, int j, int in, float r) {
 // One block per (low-res row i, sample n).  The mean-normalisation constant is reduced once
 // per block; the row's full-res support rows are contracted column-wise into LDS (coalesced
 // reads of g), then each low-res column contracts its support columns from LDS.
-__global__ __launch_bounds__(256) void up_adjoint_kernel(UpAdjArgs a) {
+// All scales in one launch: grid (max dh, N, nscales); rows past a scale's dh exit at once.
+__global__ __launch_bounds__(256) void up_adjoint_kernel(UpAdjBatch b) {
   extern __shared__ float s_col[];           // [W]
   __shared__ float s_red[2][4];
+  const UpAdjArgs a = b.s[blockIdx.z];
   const int W = a.W, H = a.H;
   const int i = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  if (i >= a.dh) return;                     // block-uniform, before any barrier
   float cn = 0.f;
   if (a.smooth_partials) {
     float m = 0.f, T = 0.f;
@@ -500,20 +508,25 @@ int launch_warp_vis(const PhotoArgs& a, int scale, const Geom& g, int C, float* 
 
 long smooth_blocks(int W, int H, int N) { return (long)cdiv(W, SM_W) * cdiv(H, SM_H) * N; }
 
-int launch_disp_sum(const float* disp, int dw, int dh, float rx, float ry, int W, int H, int N,
-                    int parts, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(disp_sum_kernel, dim3(parts, N), dim3(256), 0, st, disp, dw, dh, rx, ry, W,
-                     H, parts, out);
+int launch_disp_sum(const DispSumBatch& b, int nscales, hipStream_t st) {
+  MD2_CHECK_ARG(nscales >= 1 && nscales <= MAX_SCALES, "disp_sum: nscales");
+  hipLaunchKernelGGL(disp_sum_kernel, dim3(b.parts, b.N, nscales), dim3(256), 0, st, b);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
 
-int launch_smooth(const SmoothArgs& a, int C, hipStream_t st) {
-  dim3 grid(cdiv(a.W, SM_W), cdiv(a.H, SM_H), a.N);
+int launch_smooth(const SmoothArgs* a, int nscales, int C, hipStream_t st) {
+  MD2_CHECK_ARG(nscales >= 1 && nscales <= MAX_SCALES, "smooth: nscales");
+  SmoothBatch b{};
+  for (int k = 0; k < nscales; ++k) {
+    MD2_CHECK_ARG(a[k].N == a[0].N && a[k].W == a[0].W && a[k].H == a[0].H, "smooth: scales differ in N/W/H");
+    b.s[k] = a[k];
+  }
+  dim3 grid(cdiv(a[0].W, SM_W), cdiv(a[0].H, SM_H), a[0].N * nscales);
   if (C == 3)
-    hipLaunchKernelGGL(smooth_kernel<3>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(smooth_kernel<3>, grid, dim3(256), 0, st, b);
   else if (C == 1)
-    hipLaunchKernelGGL(smooth_kernel<1>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(smooth_kernel<1>, grid, dim3(256), 0, st, b);
   else {
     set_error("smooth: channels must be 1 or 3");
     return MD2_ENOTSUP;
@@ -522,11 +535,20 @@ int launch_smooth(const SmoothArgs& a, int C, hipStream_t st) {
   return MD2_OK;
 }
 
-int launch_up_adjoint(const UpAdjArgs& a, hipStream_t st) {
-  const bool direct = a.dw == a.W && a.dh == a.H;
-  const size_t lds = direct ? 0 : (size_t)a.W * sizeof(float);
+int launch_up_adjoint(const UpAdjArgs* a, int nscales, hipStream_t st) {
+  MD2_CHECK_ARG(nscales >= 1 && nscales <= MAX_SCALES, "up_adjoint: nscales");
+  UpAdjBatch b{};
+  int maxdh = 1;
+  bool any_lds = false;
+  for (int k = 0; k < nscales; ++k) {
+    MD2_CHECK_ARG(a[k].N == a[0].N && a[k].W == a[0].W, "up_adjoint: scales differ in N/W");
+    b.s[k] = a[k];
+    maxdh = std::max(maxdh, a[k].dh);
+    any_lds |= !(a[k].dw == a[k].W && a[k].dh == a[k].H);
+  }
+  const size_t lds = any_lds ? (size_t)a[0].W * sizeof(float) : 0;
   MD2_CHECK_ARG(lds <= 64 * 1024, "up_adjoint: full-res width exceeds the LDS row");
-  hipLaunchKernelGGL(up_adjoint_kernel, dim3(a.dh, a.N), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(up_adjoint_kernel, dim3(maxdh, a[0].N, nscales), dim3(256), lds, st, b);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }

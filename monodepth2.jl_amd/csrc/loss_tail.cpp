@@ -93,6 +93,11 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
   pa.wloss = up / ((float)c.N * c.W * c.H);
   pa.N = c.N;
   const size_t plane = (size_t)c.N * c.W * c.H;
+  DispSumBatch db{};
+  db.W = c.W;
+  db.H = c.H;
+  db.N = c.N;
+  db.parts = MEAN_PARTS;
   for (int s = 0; s < c.nscales; ++s) {
     MD2_CHECK_ARG(c.dw[s] >= 1 && c.dh[s] >= 1 && c.dw[s] <= c.W && c.dh[s] <= c.H, "scale dims");
     PhotoScale& ps = pa.sc[s];
@@ -105,19 +110,24 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     ps.partials = (float*)(ws + L.photo[s]);
     ps.loss_map = o.vis_loss ? o.vis_loss + s * plane : nullptr;
     ps.sel_map = o.vis_sel ? o.vis_sel + s * plane : nullptr;
-    MD2_TRY(launch_disp_sum(disp[s], c.dw[s], c.dh[s], ps.rx, ps.ry, c.W, c.H, c.N, MEAN_PARTS,
-                            mean + (size_t)s * c.N * MEAN_PARTS, st));
+    db.s[s] = DispSumArgs{disp[s], c.dw[s], c.dh[s], ps.rx, ps.ry, mean + (size_t)s * c.N * MEAN_PARTS};
   }
+  MD2_TRY(launch_disp_sum(db, c.nscales, st));   // every scale's mean in one launch
   if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[0], st));
   MD2_TRY(launch_photometric(pa, g, c.C, st));
   if (o.photo_events) MD2_HIP(hipEventRecord(o.photo_events[1], st));
   if (o.vis_warped) MD2_TRY(launch_warp_vis(pa, c.nscales - 1, g, c.C, o.vis_warped, st));
 
+  // smoothness and the upsample adjoint: every scale in one launch each (scale = grid z)
+  SmoothArgs sas[MAX_SCALES];
+  UpAdjArgs uas[MAX_SCALES];
+  int nua = 0;
   for (int s = 0; s < c.nscales; ++s) {
     const PhotoScale& ps = pa.sc[s];
     float* mp = mean + (size_t)s * c.N * MEAN_PARTS;
     float* sp = (float*)(ws + L.smooth[s]);
-    SmoothArgs sa{};
+    SmoothArgs& sa = sas[s];
+    sa = SmoothArgs{};
     sa.disp = disp[s];
     sa.dw = c.dw[s];
     sa.dh = c.dh[s];
@@ -133,7 +143,6 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     sa.N = c.N;
     sa.W = c.W;
     sa.H = c.H;
-    MD2_TRY(launch_smooth(sa, c.C, st));
 
     UpAdjArgs ua{};
     ua.g_full = ps.g_disp;
@@ -153,7 +162,7 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     ua.N = c.N;
     ua.W = c.W;
     ua.H = c.H;
-    if (d_disp[s]) MD2_TRY(launch_up_adjoint(ua, st));
+    if (d_disp[s]) uas[nua++] = ua;
 
     fa.photo_partials[s] = ps.partials;
     fa.photo_blocks[s] = photo_blk;
@@ -161,6 +170,8 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     fa.smooth_blocks[s] = smooth_blk;
     fa.smooth_scale[s] = c.smooth_w[s];
   }
+  MD2_TRY(launch_smooth(sas, c.nscales, c.C, st));
+  if (nua > 0) MD2_TRY(launch_up_adjoint(uas, nua, st));
   MD2_TRY(launch_loss_finalize(fa, d_pose ? dRt : nullptr, loss, st));
   if (d_pose) MD2_TRY(launch_so3_bwd(pose, 2 * c.N, c.N, c.invert_mask, dRt, d_pose, 0, st));
   return MD2_OK;
@@ -234,7 +245,7 @@ int warp_op_run(const WarpOpCfg& c, const float* disp, const float* Rt, const fl
     ua.N = c.N;
     ua.W = c.W;
     ua.H = c.H;
-    MD2_TRY(launch_up_adjoint(ua, st));
+    MD2_TRY(launch_up_adjoint(&ua, 1, st));
   }
   if (d_Rt) {
     FinalizeArgs fa{};

@@ -607,7 +607,7 @@ static int smooth_run(const float* disp, const float* img, int n, int c, int h, 
   sa.N = n;
   sa.W = w;
   sa.H = h;
-  MD2_TRY(launch_smooth(sa, c, st));
+  MD2_TRY(launch_smooth(&sa, 1, c, st));
   if (loss) {
     const int nb = (int)smooth_blocks(w, h, n);
     hipLaunchKernelGGL(reduce_partials_kernel, dim3(1, 1), dim3(256), 0, st, part, nb, 1, 2, loss,
