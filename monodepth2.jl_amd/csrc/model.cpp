@@ -619,6 +619,21 @@ class Model {
     prof_end(e, c.cat, conv_flops(s), st, "fwd", &s);
     return bn_fwd(bn, y, nimg, HW, st, slot);
   }
+  // MD2_FUSE_SKIP_BWD=0 restores the axpy of the decoder skip gradients (A/B, bit-identity test)
+  const bool fuse_skip_bwd = [] {
+    const char* v = getenv("MD2_FUSE_SKIP_BWD");
+    return !(v && v[0] == '0');
+  }();
+  // MD2_FUSE_POOL_FWD=0 restores bn_apply_fused + maxpool_fwd for the stem (A/B, bit-identity test)
+  const bool fuse_pool_fwd = [] {
+    const char* v = getenv("MD2_FUSE_POOL_FWD");
+    return !(v && v[0] == '0');
+  }();
+  // MD2_FUSE_POOL_BWD=0 restores maxpool_bwd + axpy + bn_bwd for the stem (A/B, bit-identity test)
+  const bool fuse_pool_bwd = [] {
+    const char* v = getenv("MD2_FUSE_POOL_BWD");
+    return !(v && v[0] == '0');
+  }();
   // MD2_FUSE_SPLITK=0 restores the separate reduction launches (A/B measurement)
   const bool fuse_splitk = [] {
     const char* v = getenv("MD2_FUSE_SPLITK");
@@ -703,8 +718,12 @@ class Model {
     MD2_TRY(conv_f_bn(stem, nimg, in, y0, 64 * hw0, stem_bn, hw0, st));
     BNApplyFused ap{};
     ap.y = y0; ap.s1 = bn_in(stem_bn); ap.relu = 1;
-    MD2_TRY(bn_apply_fused(ap, f0, nimg, 64, hw0, st));
-    MD2_TRY(maxpool_fwd(f0, nimg, 64, H0, W0, mp, mp_arg, Hm, Wm, st));
+    if (H0 % 2 == 0 && W0 % 2 == 0 && fuse_pool_fwd) {   // BN + ReLU + max pool in one pass
+      MD2_TRY(bn_relu_maxpool(ap, f0, nimg, 64, H0, W0, mp, mp_arg, Hm, Wm, st));
+    } else {
+      MD2_TRY(bn_apply_fused(ap, f0, nimg, 64, hw0, st));
+      MD2_TRY(maxpool_fwd(f0, nimg, 64, H0, W0, mp, mp_arg, Hm, Wm, st));
+    }
     for (auto& sg : stages)
       for (auto& b : sg) {
         const float* x = b.in;
@@ -947,24 +966,40 @@ class Model {
   // mask: the BN+ReLU output whose ReLU gates dout, or nullptr with relu_from_y for a residual-free
   // BN+ReLU (stem, intra-block): the mask is re-derived from y (bit-exact, one read less)
   int bn_bwd(RBN& bn, const float* dout, const float* mask, const float* y, int nimg, long HW,
-             float* dy, float* dres, int dres_acc, hipStream_t st, bool relu_from_y = false) {
+             float* dy, float* dres, int dres_acc, hipStream_t st, bool relu_from_y = false,
+             SkipAdd sk = SkipAdd{}) {
     BNStatsWs w = bnws;
     w.parts = bn_parts(bn.p.c, nimg, HW);
     const float* mg = relu_from_y ? P(bn.p.g) : nullptr;
     const float* mb = relu_from_y ? P(bn.p.b) : nullptr;
     if (relu_from_y) mask = nullptr;
-    MD2_TRY(bn_bwd_partial(dout, mask, y, bn.mean, bn.invstd, nimg, bn.p.c, HW, w, st, mg, mb));
+    MD2_TRY(bn_bwd_partial(dout, mask, y, bn.mean, bn.invstd, nimg, bn.p.c, HW, w, st, mg, mb, sk));
     return bn_bwd_apply_fused(dout, mask, y, bn.mean, bn.invstd, P(bn.p.g), w, Gd(bn.p.g),
-                              Gd(bn.p.b), nimg, bn.p.c, HW, dy, dres, dres_acc, st, mb);
+                              Gd(bn.p.b), nimg, bn.p.c, HW, dy, dres, dres_acc, st, mb, sk);
+  }
+  // the decoder skip gradient d_skip[si] on the target slice of encoder feature si (si = 1..3, the
+  // input of stage si = the output of stage si-1): added by stage si-1's last-block BN backward
+  // when fused (MD2_FUSE_SKIP_BWD, HW % 4 == 0), else by an axpy after stage si's backward
+  bool skip_fused(int si) const {
+    return fuse_skip_bwd && si >= 1 && si <= 3 && d_skip[si] && ((long)featH[si] * featW[si]) % 4 == 0;
+  }
+  SkipAdd skip_add(int si) const {
+    SkipAdd sk;
+    if (!skip_fused(si)) return sk;
+    const long fsz = (long)featC[si] * featH[si] * featW[si];
+    sk.skip = d_skip[si];
+    sk.lo = (long)T0 * fsz;
+    sk.hi = (long)(T0 + N) * fsz;
+    return sk;
   }
 
-  int block_bwd(EncBlock& b, hipStream_t st) {
+  int block_bwd(EncBlock& b, hipStream_t st, SkipAdd sk = SkipAdd{}) {
     const int nimg = B;
     const long ohw = (long)b.H * b.W, ihw = (long)b.Hin * b.Win;
     const int ns = (int)b.st.size();
     EncStage& last = b.st.back();
-    // last BN (+ residual, ReLU): g = d_out * relu'(out)
-    MD2_TRY(bn_bwd(last.bn, b.d_out, last.a, last.y, nimg, ohw, DY, b.down ? G : b.d_in, 0, st));
+    // last BN (+ residual, ReLU): g = (d_out [+ skip]) * relu'(out)
+    MD2_TRY(bn_bwd(last.bn, b.d_out, last.a, last.y, nimg, ohw, DY, b.down ? G : b.d_in, 0, st, false, sk));
     if (b.down) {
       MD2_TRY(bn_bwd(b.dbn, G, nullptr, b.yd, nimg, ohw, DYD, nullptr, 0, st));
       MD2_TRY(conv_wd(b.dconv, nimg, tin(b.in, b.Cin, ihw), DYD, b.d_in, (long)b.Cin * ihw, 0, st));
@@ -1043,8 +1078,9 @@ class Model {
 
   int seg_stage(int si, hipStream_t st) {
     auto& sg = stages[si];
-    for (int k = (int)sg.size() - 1; k >= 0; --k) MD2_TRY(block_bwd(sg[k], st));
-    if (si >= 1) {
+    for (int k = (int)sg.size() - 1; k >= 0; --k)
+      MD2_TRY(block_bwd(sg[k], st, k == (int)sg.size() - 1 ? skip_add(si + 1) : SkipAdd{}));
+    if (si >= 1 && !skip_fused(si)) {
       // d f_si (= block 0's d_in) += decoder skip gradient on the target slice
       const long n = (long)N * featC[si] * featH[si] * featW[si];
       MD2_TRY(axpy(sg[0].d_in + (long)T0 * featC[si] * featH[si] * featW[si], d_skip[si], n, st));
@@ -1054,10 +1090,20 @@ class Model {
 
   int seg_stem(hipStream_t st) {
     const long hw0 = (long)H0 * W0;
-    MD2_TRY(maxpool_bwd(d_mp, mp_arg, B, 64, H0, W0, Hm, Wm, d_f0, st));
-    const long n = (long)N * 64 * hw0;
-    MD2_TRY(axpy(d_f0 + (long)T0 * 64 * hw0, d_skip[0], n, st));
-    MD2_TRY(bn_bwd(stem_bn, d_f0, f0, y0, B, hw0, DY, nullptr, 0, st, true));
+    if (W0 % 4 == 0 && fuse_pool_bwd) {
+      // max-pool adjoint + skip gradient formed inside both BN-backward passes (d_f0 is not
+      // materialised; bit-identical to the three-launch path below)
+      BNStatsWs w = bnws;
+      w.parts = bn_parts(64, B, hw0);
+      MD2_TRY(bn_bwd_pool(d_mp, mp_arg, Hm, Wm, d_skip[0], T0, N, y0, stem_bn.mean, stem_bn.invstd,
+                          P(stem_bn.p.g), P(stem_bn.p.b), B, 64, H0, W0, w, Gd(stem_bn.p.g),
+                          Gd(stem_bn.p.b), DY, st));
+    } else {
+      MD2_TRY(maxpool_bwd(d_mp, mp_arg, B, 64, H0, W0, Hm, Wm, d_f0, st));
+      const long n = (long)N * 64 * hw0;
+      MD2_TRY(axpy(d_f0 + (long)T0 * 64 * hw0, d_skip[0], n, st));
+      MD2_TRY(bn_bwd(stem_bn, d_f0, f0, y0, B, hw0, DY, nullptr, 0, st, true));
+    }
     const long fs = (long)cfg.arch.in_ch * cfg.H * cfg.W;
     TensorIn in;
     in.p0 = cur_x;
@@ -1274,7 +1320,8 @@ int model_debug_tensor(Model* m, int index, const char** name, const void** ptr,
       ts.push_back({"d_skip" + std::to_string(f), m->d_skip[f], N, m->featC[f], m->featH[f],
                     m->featW[f], 0});
   ts.push_back({"d_mp", m->d_mp, B, 64, m->Hm, m->Wm, 0});
-  ts.push_back({"d_f0", m->d_f0, B, 64, m->H0, m->W0, 0});
+  if (!m->fuse_pool_bwd || m->W0 % 4 != 0)   // not materialised by the fused stem backward
+    ts.push_back({"d_f0", m->d_f0, B, 64, m->H0, m->W0, 0});
   if (index < 0 || index >= (int)ts.size()) {
     set_error("debug_tensor: index out of range");
     return MD2_EINVAL;

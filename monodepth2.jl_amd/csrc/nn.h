@@ -19,6 +19,20 @@ struct SlabIn {
   const float* slab = nullptr;
   int splits = 0;
 };
+// optional addend of a BN backward's dout: skip[e - lo] over flat elements [lo, hi)
+struct SkipAdd {
+  const float* skip = nullptr;
+  long lo = 0, hi = 0;
+};
+// the max-pool adjoint source of bn_bwd_pool (see pool_dout4 in nn.hip)
+struct PoolDout {
+  const float* dmp = nullptr;          // [N][C][Ho][Wo] pooled gradient
+  const unsigned char* arg = nullptr;  // window argmax 0..8
+  const float* skip = nullptr;         // added over flat elements [skip_lo, skip_hi)
+  uint32_t skip_lo = 0, skip_hi = 0;
+  int Ho = 0, Wo = 0;
+  FastDiv fdW{}, fdHW{};
+};
 // mean/invstd [C]; running stats updated when run_mean != nullptr (momentum, unbiased var)
 int bn_stats(const float* y, int N, int C, long HW, float eps, float momentum, float* mean,
              float* invstd, float* run_mean, float* run_var, BNStatsWs ws, hipStream_t st);
@@ -63,7 +77,7 @@ int bn_bwd_reduce(const float* dout, const float* mask_out, const float* y, cons
 // re-derived from y bit-exactly (bn_apply_fused's explicit roundings) instead of read back
 int bn_bwd_partial(const float* dout, const float* mask_out, const float* y, const float* mean,
                    const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st,
-                   const float* mgamma = nullptr, const float* mbeta = nullptr);
+                   const float* mgamma = nullptr, const float* mbeta = nullptr, SkipAdd sk = SkipAdd{});
 // the same with dout formed from the dgrad's split-K slabs (and written to dout)
 int bn_bwd_partial_slabs(SlabIn sl, float* dout, const float* y, const float* mean,
                          const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st,
@@ -71,7 +85,8 @@ int bn_bwd_partial_slabs(SlabIn sl, float* dout, const float* y, const float* me
 int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y, const float* mean,
                        const float* invstd, const float* gamma, BNStatsWs ws, float* dgamma,
                        float* dbeta, int N, int C, long HW, float* dy, float* dres,
-                       int dres_accumulate, hipStream_t st, const float* mbeta = nullptr);
+                       int dres_accumulate, hipStream_t st, const float* mbeta = nullptr,
+                       SkipAdd sk = SkipAdd{});
 // dy = gamma*invstd*(g - dbeta/L - xhat*dgamma/L); optional dres (=g) store/accumulate
 int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const float* mean,
                  const float* invstd, const float* gamma, const float* dgamma,
@@ -79,6 +94,17 @@ int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const
                  int dres_accumulate, hipStream_t st);
 
 // ---- MaxPool((3,3); stride 2, pad 1) ----
+// backward of the stem BN+ReLU feeding the 3x3/2 max pool: dout = maxpool adjoint of dmp (argmax
+// `arg`) plus, over images [skip_img0, skip_img0+skip_nimg), the decoder skip gradient -- formed
+// in-kernel (never materialised); ReLU mask from y; W % 4 == 0
+int bn_bwd_pool(const float* dmp, const unsigned char* arg, int Ho, int Wo, const float* skip,
+                int skip_img0, int skip_nimg, const float* y, const float* mean, const float* invstd,
+                const float* gamma, const float* beta, int N, int C, int H, int W, BNStatsWs ws,
+                float* dgamma, float* dbeta, float* dy, hipStream_t st);
+// stem tail: act = relu(BN(p.y)) (statistics finalised from p.s1's partials) and its 3x3/2/pad-1
+// max pool (y, argmax) in one pass; even H, W; bit-identical to bn_apply_fused + maxpool_fwd
+int bn_relu_maxpool(const BNApplyFused& p, float* act, int N, int C, int H, int W, float* y,
+                    unsigned char* arg, int Ho, int Wo, hipStream_t st);
 int maxpool_fwd(const float* x, int N, int C, int H, int W, float* y, unsigned char* arg,
                 int Ho, int Wo, hipStream_t st);
 int maxpool_bwd(const float* dy, const unsigned char* arg, int N, int C, int H, int W, int Ho,

@@ -360,13 +360,68 @@ __device__ __forceinline__ float ymasked(float g, float y, const YMask& m) {
   return (m.on && !(__fmaf_rn(y, m.sc, m.sh) > 0.f)) ? 0.f : g;
 }
 
+// POOL: dout is not read but formed on the fly as the max-pool adjoint of the pooled gradient
+// (the stem: maxpool_bwd_kernel's 2x2-block sums, same terms, same order) plus the decoder's skip
+// gradient over the target images (axpy's d_f0 += d_skip) -- bit-identical to materialising
+// d_f0, which is then never written nor read (two full passes over the stem-sized tensor less)
+__device__ __forceinline__ float4 pool_dout4(const PoolDout& q, uint32_t i) {
+  const uint32_t plane = fdiv(i, q.fdHW);
+  const uint32_t pix = i - plane * q.fdHW.d;
+  const uint32_t h = fdiv(pix, q.fdW);
+  const int w0 = (int)(pix - h * q.fdW.d);          // multiple of 4
+  const int oi = (int)(h >> 1), j0 = w0 >> 1;
+  const bool odd = h & 1u;
+  const bool hasr = oi + 1 < q.Ho;
+  const uint32_t o = plane * (uint32_t)(q.Ho * q.Wo) + (uint32_t)(oi * q.Wo + j0);
+  int a0[3], a1[3];
+  float g0[3], g1[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const bool c = j0 + t < q.Wo;
+    a0[t] = c ? (int)q.arg[o + t] : -1;
+    g0[t] = c ? q.dmp[o + t] : 0.f;
+    a1[t] = (odd && hasr && c) ? (int)q.arg[o + q.Wo + t] : -1;
+    g1[t] = (odd && hasr && c) ? q.dmp[o + q.Wo + t] : 0.f;
+  }
+  float e[4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {   // pooled column j0 + t owns elements 2(j0+t), 2(j0+t)+1
+    if (!odd) {
+      e[2 * t] = a0[t] == 4 ? g0[t] : 0.f;
+      e[2 * t + 1] = (a0[t] == 5 ? g0[t] : 0.f) + (a0[t + 1] == 3 ? g0[t + 1] : 0.f);
+    } else {
+      e[2 * t] = (a0[t] == 7 ? g0[t] : 0.f) + (a1[t] == 1 ? g1[t] : 0.f);
+      e[2 * t + 1] = (a0[t] == 8 ? g0[t] : 0.f) + (a0[t + 1] == 6 ? g0[t + 1] : 0.f) +
+                     (a1[t] == 2 ? g1[t] : 0.f) + (a1[t + 1] == 0 ? g1[t + 1] : 0.f);
+    }
+  }
+  if (q.skip && i >= q.skip_lo && i < q.skip_hi) {
+    const float4 k = *reinterpret_cast<const float4*>(q.skip + (i - q.skip_lo));
+    e[0] += k.x; e[1] += k.y; e[2] += k.z; e[3] += k.w;
+  }
+  return make_float4(e[0], e[1], e[2], e[3]);
+}
+
+__device__ __forceinline__ float4 add_skip4(const PoolDout& q, uint32_t i, float4 g) {
+  if (i >= q.skip_lo && i < q.skip_hi) {
+    const float4 k = *reinterpret_cast<const float4*>(q.skip + (i - q.skip_lo));
+    g.x += k.x; g.y += k.y; g.z += k.z; g.w += k.w;
+  }
+  return g;
+}
+
 // SLAB: dout formed from the dgrad conv's split-K slabs and written (see bn_stats_partial_kernel)
-template <bool VEC, bool SLAB = false>
+// SKIP: dout + pd.skip over flat elements [pd.skip_lo, pd.skip_hi) (the decoder skip gradient,
+// added where axpy used to add it before this pass; same fp add, bit-identical)
+template <bool VEC, bool SLAB = false, bool POOL = false, bool SKIP = false>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ mgamma,
     const float* __restrict__ mbeta, int C, int HW, int N, int parts, FastDiv fdu,
-    double* __restrict__ part, SlabIn sl = SlabIn{}, float* __restrict__ dout_w = nullptr) {
+    double* __restrict__ part, SlabIn sl = SlabIn{}, float* __restrict__ dout_w = nullptr,
+    PoolDout pd = PoolDout{}) {
+  static_assert(!POOL || (VEC && !SLAB), "POOL: float4 units, no slabs");
+  static_assert(!SKIP || (VEC && !SLAB && !POOL), "SKIP: float4 units of a read dout");
   __shared__ double red[8];
   const int c = blockIdx.x, p = blockIdx.y;
   const int i0 = (int)((long)N * p / parts), i1 = (int)((long)N * (p + 1) / parts);
@@ -405,7 +460,11 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
       }
       if (VEC) {
         const long i = base + 4 * k;
-        if (!SLAB) gv[h] = *reinterpret_cast<const float4*>(dout + i);
+        if (POOL)
+          gv[h] = pool_dout4(pd, (uint32_t)i);
+        else if (!SLAB)
+          gv[h] = *reinterpret_cast<const float4*>(dout + i);
+        if (SKIP) gv[h] = add_skip4(pd, (uint32_t)i, gv[h]);
         yv[h] = *reinterpret_cast<const float4*>(y + i);
         if (mask) {
           const float4 m = *reinterpret_cast<const float4*>(mask + i);
@@ -468,14 +527,28 @@ __global__ void bn_bwd_final_kernel(const double* __restrict__ part, int C, int 
   dgamma[c] = (float)sgx;
 }
 
+static PoolDout skip_src(const SkipAdd& sk) {
+  PoolDout pd{};
+  pd.skip = sk.skip;
+  pd.skip_lo = (uint32_t)sk.lo;
+  pd.skip_hi = (uint32_t)sk.hi;
+  return pd;
+}
+
 int bn_bwd_partial(const float* dout, const float* mask_out, const float* y, const float* mean,
                    const float* invstd, int N, int C, long HW, BNStatsWs ws, hipStream_t st,
-                   const float* mgamma, const float* mbeta) {
+                   const float* mgamma, const float* mbeta, SkipAdd sk) {
   MD2_TRY(check_u31((long)N * C * HW));
   MD2_CHECK_ARG(ws.parts >= 1 && ws.parts <= N, "bn_bwd: parts must split the images");
   const int vec = HW % 4 == 0;
   const FastDiv fdu = fd(vec ? HW / 4 : HW);
-  if (vec)
+  MD2_CHECK_ARG(!sk.skip || (vec && sk.lo >= 0 && sk.lo <= sk.hi && sk.hi <= (long)N * C * HW),
+                "bn_bwd: skip range / HW % 4");
+  if (sk.skip)
+    hipLaunchKernelGGL((bn_bwd_partial_kernel<true, false, false, true>), dim3(C, ws.parts), dim3(256), 0,
+                       st, dout, mask_out, y, mean, invstd, mgamma, mbeta, C, (int)HW, N, ws.parts, fdu,
+                       ws.partials, SlabIn{}, (float*)nullptr, skip_src(sk));
+  else if (vec)
     hipLaunchKernelGGL(bn_bwd_partial_kernel<true>, dim3(C, ws.parts), dim3(256), 0, st, dout,
                        mask_out, y, mean, invstd, mgamma, mbeta, C, (int)HW, N, ws.parts, fdu,
                        ws.partials);
@@ -606,14 +679,16 @@ int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const
 // ---- fused finalise + backward apply: per block the channels of its planes sum the backward
 // partials in bn_bwd_final_kernel's order (bit-identical dgamma/dbeta), the owner block of each
 // channel (first unit of image 0's plane) stores dgamma[c]/dbeta[c].
-template <bool VEC>
+template <bool VEC, bool POOL = false, bool SKIP = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const double* __restrict__ part, int parts,
     float* __restrict__ dgamma, float* __restrict__ dbeta, uint32_t nu, FastDiv fdU, FastDiv fdC,
     float invL, float* __restrict__ dy, float* __restrict__ dres, int dres_acc,
-    const float* __restrict__ mbeta) {
+    const float* __restrict__ mbeta, PoolDout pd = PoolDout{}) {
+  static_assert(!POOL || VEC, "POOL: float4 units");
+  static_assert(!SKIP || (VEC && !POOL), "SKIP: float4 units of a read dout");
   __shared__ float s_k0[256], s_db[256], s_dg[256], s_mu[256], s_is[256], s_msc[256], s_msh[256];
   const uint32_t u0 = blockIdx.x * 256u;
   const uint32_t pl0 = fdiv(u0, fdU);
@@ -656,7 +731,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
     const long i = 4L * u;
     float g[4];
     {
-      const float4 t = *reinterpret_cast<const float4*>(dout + i);
+      float4 t = POOL ? pool_dout4(pd, (uint32_t)i) : *reinterpret_cast<const float4*>(dout + i);
+      if (SKIP) t = add_skip4(pd, (uint32_t)i, t);
       g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
     }
     if (mask) {
@@ -700,12 +776,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
 int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y, const float* mean,
                        const float* invstd, const float* gamma, BNStatsWs ws, float* dgamma,
                        float* dbeta, int N, int C, long HW, float* dy, float* dres,
-                       int dres_accumulate, hipStream_t st, const float* mbeta) {
+                       int dres_accumulate, hipStream_t st, const float* mbeta, SkipAdd sk) {
   const long n = (long)N * C * HW;
   MD2_TRY(check_u31(n));
   MD2_CHECK_ARG(ws.partials && ws.parts >= 1, "bn_bwd_apply_fused: missing partials");
+  MD2_CHECK_ARG(!sk.skip || (HW % 4 == 0 && sk.lo >= 0 && sk.lo <= sk.hi && sk.hi <= n),
+                "bn_bwd: skip range / HW % 4");
   const float invL = 1.f / (float)((long)N * HW);
-  if (HW % 4 == 0)
+  if (sk.skip)
+    hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<true, false, true>), dim3(cdiv(n / 4, 256)), dim3(256), 0,
+                       st, dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
+                       (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy, dres, dres_accumulate, mbeta,
+                       skip_src(sk));
+  else if (HW % 4 == 0)
     hipLaunchKernelGGL(bn_bwd_apply_fused_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st,
                        dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
                        (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy, dres, dres_accumulate, mbeta);
@@ -713,6 +796,42 @@ int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y,
     hipLaunchKernelGGL(bn_bwd_apply_fused_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st,
                        dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
                        (uint32_t)n, fd(HW), fd(C), invL, dy, dres, dres_accumulate, mbeta);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// backward of the stem BN+ReLU whose output fed the 3x3/2 max pool (and, for images
+// [skip_img0, skip_img0 + skip_nimg), the decoder skip): dout = maxpool adjoint of dmp (+ skip)
+// formed inside both passes (POOL), the ReLU mask re-derived from y
+int bn_bwd_pool(const float* dmp, const unsigned char* arg, int Ho, int Wo, const float* skip,
+                int skip_img0, int skip_nimg, const float* y, const float* mean, const float* invstd,
+                const float* gamma, const float* beta, int N, int C, int H, int W, BNStatsWs ws,
+                float* dgamma, float* dbeta, float* dy, hipStream_t st) {
+  const long HW = (long)H * W;
+  MD2_TRY(check_u31((long)N * C * HW));
+  MD2_CHECK_ARG(W % 4 == 0 && Ho == (H + 1) / 2 && Wo == (W + 1) / 2, "bn_bwd_pool: W % 4, pool shape");
+  MD2_CHECK_ARG(ws.partials && ws.parts >= 1 && ws.parts <= N, "bn_bwd_pool: parts must split the images");
+  MD2_CHECK_ARG(!skip || (skip_img0 >= 0 && skip_img0 + skip_nimg <= N), "bn_bwd_pool: skip images");
+  PoolDout pd{};
+  pd.dmp = dmp;
+  pd.arg = arg;
+  pd.skip = skip;
+  pd.skip_lo = (uint32_t)((long)skip_img0 * C * HW);
+  pd.skip_hi = (uint32_t)((long)(skip_img0 + skip_nimg) * C * HW);
+  pd.Ho = Ho;
+  pd.Wo = Wo;
+  pd.fdW = fd(W);
+  pd.fdHW = fd(HW);
+  hipLaunchKernelGGL((bn_bwd_partial_kernel<true, false, true>), dim3(C, ws.parts), dim3(256), 0, st,
+                     (const float*)nullptr, (const float*)nullptr, y, mean, invstd, gamma, beta, C,
+                     (int)HW, N, ws.parts, fd(HW / 4), ws.partials, SlabIn{}, (float*)nullptr, pd);
+  MD2_LAUNCH_CHECK();
+  const long n = (long)N * C * HW;
+  const float invL = 1.f / (float)((long)N * HW);
+  hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<true, true>), dim3(cdiv(n / 4, 256)), dim3(256), 0, st,
+                     (const float*)nullptr, (const float*)nullptr, y, mean, invstd, gamma, ws.partials,
+                     ws.parts, dgamma, dbeta, (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy,
+                     (float*)nullptr, 0, beta, pd);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -798,6 +917,78 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
       if (2 * j + 1 < W) q[W + 1] = e11;
     }
   }
+}
+
+// ResNet stem tail in one pass: BN (batch statistics finalised per block, bn_apply_fused's
+// explicit roundings) + ReLU + MaxPool 3x3/2/pad 1.  One pooled output per thread: it evaluates
+// relu(fma(y, sc, sh)) over its window (bit-identical to bn_apply_fused then maxpool_fwd), stores
+// the window's own 2x2 block of the activation (rows 2oh..2oh+1, columns 2ow..2ow+1: every
+// activation exactly once, even H and W) and the max / argmax -- the activation is written but
+// never read back (the pool used to re-read it: one full read of the stem output less).
+__global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(BNApplyFused p, float* __restrict__ act,
+                                                              int H, int W, float* __restrict__ y,
+                                                              unsigned char* __restrict__ arg,
+                                                              FastDiv fdWo, FastDiv fdHo, FastDiv fdU,
+                                                              FastDiv fdC, uint32_t n, double total) {
+  __shared__ float s_sc[256], s_sh[256];
+  const uint32_t u0 = blockIdx.x * 256u;
+  const uint32_t pl0 = fdiv(u0, fdU);
+  const uint32_t npl = fdiv(min(u0 + 255u, n - 1u), fdU) - pl0 + 1u;
+  for (uint32_t t = threadIdx.x >> 6; t < npl; t += 4) {   // wave-uniform plane loop
+    const uint32_t pl = pl0 + t;
+    const int c = (int)(pl - fdiv(pl, fdC) * fdC.d);
+    const bool owner = pl < fdC.d && pl * fdU.d >= u0;
+    float sc, sh;
+    bn_finalise_plane(p.s1, c, total, owner, sc, sh);
+    if ((threadIdx.x & 63) == 0) {
+      s_sc[t] = sc;
+      s_sh[t] = sh;
+    }
+  }
+  __syncthreads();
+  const uint32_t i = u0 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = fdiv(i, fdWo), plane = fdiv(r, fdHo);
+  const int ow = (int)(i - r * fdWo.d), oh = (int)(r - plane * fdHo.d);
+  const float sc = s_sc[plane - pl0], sh = s_sh[plane - pl0];
+  const uint32_t base = plane * (uint32_t)(H * W);
+  const float* src = p.y + base;
+  float best = -INFINITY;
+  int bi = 0;
+  const int iw = ow * 2;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int ih = oh * 2 - 1 + kh;
+    if (ih < 0) continue;                       // ih <= 2*oh + 1 < H (even H)
+    const float* row = src + ih * W;
+    float v0 = -INFINITY;
+    if (iw > 0) v0 = fmaxf(__fmaf_rn(row[iw - 1], sc, sh), 0.f);
+    const float2 t = *reinterpret_cast<const float2*>(row + iw);
+    const float v1 = fmaxf(__fmaf_rn(t.x, sc, sh), 0.f);
+    const float v2 = fmaxf(__fmaf_rn(t.y, sc, sh), 0.f);
+    if (kh > 0) *reinterpret_cast<float2*>(act + base + ih * W + iw) = make_float2(v1, v2);
+    // strict '>' in (kh, kw) scan order: the first maximum wins (NNlib maxpool)
+    if (v0 > best) { best = v0; bi = kh * 3; }
+    if (v1 > best) { best = v1; bi = kh * 3 + 1; }
+    if (v2 > best) { best = v2; bi = kh * 3 + 2; }
+  }
+  y[i] = best;
+  arg[i] = (unsigned char)bi;
+}
+
+int bn_relu_maxpool(const BNApplyFused& p, float* act, int N, int C, int H, int W, float* y,
+                    unsigned char* arg, int Ho, int Wo, hipStream_t st) {
+  MD2_CHECK_ARG(H % 2 == 0 && W % 2 == 0 && Ho == H / 2 && Wo == W / 2,
+                "bn_relu_maxpool: even input, 3x3/2 pad-1 output shape");
+  MD2_CHECK_ARG(p.y && p.s1.part && p.s1.parts >= 1 && !p.y2 && !p.res && p.relu,
+                "bn_relu_maxpool: BN+ReLU without residual / second branch");
+  const long n = (long)N * C * Ho * Wo;
+  MD2_TRY(check_u31((long)N * C * H * W));
+  const double total = (double)((long)N * H * W);
+  hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, p, act, H, W, y,
+                     arg, fd(Wo), fd(Ho), fd((long)Ho * Wo), fd(C), (uint32_t)n, total);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
 }
 
 int maxpool_fwd(const float* x, int N, int C, int H, int W, float* y, unsigned char* arg, int Ho,
