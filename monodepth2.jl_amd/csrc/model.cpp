@@ -629,7 +629,8 @@ class Model {
     const char* v = getenv("MD2_FUSE_POOL_FWD");
     return !(v && v[0] == '0');
   }();
-  // MD2_FUSE_POOL_BWD=0 restores maxpool_bwd + axpy + bn_bwd for the stem (A/B, bit-identity test)
+  // MD2_FUSE_POOL_BWD=0 restores the stem's separate skip-gradient axpy after maxpool_bwd (A/B,
+  // bit-identity test)
   const bool fuse_pool_bwd = [] {
     const char* v = getenv("MD2_FUSE_POOL_BWD");
     return !(v && v[0] == '0');
@@ -1090,20 +1091,19 @@ class Model {
 
   int seg_stem(hipStream_t st) {
     const long hw0 = (long)H0 * W0;
-    if (W0 % 4 == 0 && fuse_pool_bwd) {
-      // max-pool adjoint + skip gradient formed inside both BN-backward passes (d_f0 is not
-      // materialised; bit-identical to the three-launch path below)
-      BNStatsWs w = bnws;
-      w.parts = bn_parts(64, B, hw0);
-      MD2_TRY(bn_bwd_pool(d_mp, mp_arg, Hm, Wm, d_skip[0], T0, N, y0, stem_bn.mean, stem_bn.invstd,
-                          P(stem_bn.p.g), P(stem_bn.p.b), B, 64, H0, W0, w, Gd(stem_bn.p.g),
-                          Gd(stem_bn.p.b), DY, st));
+    const long n = (long)N * 64 * hw0;
+    if (W0 % 2 == 0 && fuse_pool_bwd && d_skip[0]) {
+      // the decoder skip gradient added by the max-pool adjoint itself (no axpy pass)
+      SkipAdd sk;
+      sk.skip = d_skip[0];
+      sk.lo = (long)T0 * 64 * hw0;
+      sk.hi = sk.lo + n;
+      MD2_TRY(maxpool_bwd(d_mp, mp_arg, B, 64, H0, W0, Hm, Wm, d_f0, st, sk));
     } else {
       MD2_TRY(maxpool_bwd(d_mp, mp_arg, B, 64, H0, W0, Hm, Wm, d_f0, st));
-      const long n = (long)N * 64 * hw0;
       MD2_TRY(axpy(d_f0 + (long)T0 * 64 * hw0, d_skip[0], n, st));
-      MD2_TRY(bn_bwd(stem_bn, d_f0, f0, y0, B, hw0, DY, nullptr, 0, st, true));
     }
+    MD2_TRY(bn_bwd(stem_bn, d_f0, f0, y0, B, hw0, DY, nullptr, 0, st, true));
     const long fs = (long)cfg.arch.in_ch * cfg.H * cfg.W;
     TensorIn in;
     in.p0 = cur_x;
@@ -1320,8 +1320,7 @@ int model_debug_tensor(Model* m, int index, const char** name, const void** ptr,
       ts.push_back({"d_skip" + std::to_string(f), m->d_skip[f], N, m->featC[f], m->featH[f],
                     m->featW[f], 0});
   ts.push_back({"d_mp", m->d_mp, B, 64, m->Hm, m->Wm, 0});
-  if (!m->fuse_pool_bwd || m->W0 % 4 != 0)   // not materialised by the fused stem backward
-    ts.push_back({"d_f0", m->d_f0, B, 64, m->H0, m->W0, 0});
+  ts.push_back({"d_f0", m->d_f0, B, 64, m->H0, m->W0, 0});
   if (index < 0 || index >= (int)ts.size()) {
     set_error("debug_tensor: index out of range");
     return MD2_EINVAL;

@@ -24,14 +24,10 @@ struct SkipAdd {
   const float* skip = nullptr;
   long lo = 0, hi = 0;
 };
-// the max-pool adjoint source of bn_bwd_pool (see pool_dout4 in nn.hip)
-struct PoolDout {
-  const float* dmp = nullptr;          // [N][C][Ho][Wo] pooled gradient
-  const unsigned char* arg = nullptr;  // window argmax 0..8
-  const float* skip = nullptr;         // added over flat elements [skip_lo, skip_hi)
+// device-side form of a SkipAdd (nn.hip)
+struct SkipSrc {
+  const float* skip = nullptr;
   uint32_t skip_lo = 0, skip_hi = 0;
-  int Ho = 0, Wo = 0;
-  FastDiv fdW{}, fdHW{};
 };
 // mean/invstd [C]; running stats updated when run_mean != nullptr (momentum, unbiased var)
 int bn_stats(const float* y, int N, int C, long HW, float eps, float momentum, float* mean,
@@ -94,21 +90,15 @@ int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const
                  int dres_accumulate, hipStream_t st);
 
 // ---- MaxPool((3,3); stride 2, pad 1) ----
-// backward of the stem BN+ReLU feeding the 3x3/2 max pool: dout = maxpool adjoint of dmp (argmax
-// `arg`) plus, over images [skip_img0, skip_img0+skip_nimg), the decoder skip gradient -- formed
-// in-kernel (never materialised); ReLU mask from y; W % 4 == 0
-int bn_bwd_pool(const float* dmp, const unsigned char* arg, int Ho, int Wo, const float* skip,
-                int skip_img0, int skip_nimg, const float* y, const float* mean, const float* invstd,
-                const float* gamma, const float* beta, int N, int C, int H, int W, BNStatsWs ws,
-                float* dgamma, float* dbeta, float* dy, hipStream_t st);
 // stem tail: act = relu(BN(p.y)) (statistics finalised from p.s1's partials) and its 3x3/2/pad-1
 // max pool (y, argmax) in one pass; even H, W; bit-identical to bn_apply_fused + maxpool_fwd
 int bn_relu_maxpool(const BNApplyFused& p, float* act, int N, int C, int H, int W, float* y,
                     unsigned char* arg, int Ho, int Wo, hipStream_t st);
 int maxpool_fwd(const float* x, int N, int C, int H, int W, float* y, unsigned char* arg,
                 int Ho, int Wo, hipStream_t st);
+// optional skip: dx += skip over whole images (the decoder skip gradient; even W)
 int maxpool_bwd(const float* dy, const unsigned char* arg, int N, int C, int H, int W, int Ho,
-                int Wo, float* dx, hipStream_t st);
+                int Wo, float* dx, hipStream_t st, SkipAdd skip = SkipAdd{});
 
 // ---- upsample_bilinear(x, (2,2)), align_corners = true ----
 int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStream_t st);

@@ -360,49 +360,7 @@ __device__ __forceinline__ float ymasked(float g, float y, const YMask& m) {
   return (m.on && !(__fmaf_rn(y, m.sc, m.sh) > 0.f)) ? 0.f : g;
 }
 
-// POOL: dout is not read but formed on the fly as the max-pool adjoint of the pooled gradient
-// (the stem: maxpool_bwd_kernel's 2x2-block sums, same terms, same order) plus the decoder's skip
-// gradient over the target images (axpy's d_f0 += d_skip) -- bit-identical to materialising
-// d_f0, which is then never written nor read (two full passes over the stem-sized tensor less)
-__device__ __forceinline__ float4 pool_dout4(const PoolDout& q, uint32_t i) {
-  const uint32_t plane = fdiv(i, q.fdHW);
-  const uint32_t pix = i - plane * q.fdHW.d;
-  const uint32_t h = fdiv(pix, q.fdW);
-  const int w0 = (int)(pix - h * q.fdW.d);          // multiple of 4
-  const int oi = (int)(h >> 1), j0 = w0 >> 1;
-  const bool odd = h & 1u;
-  const bool hasr = oi + 1 < q.Ho;
-  const uint32_t o = plane * (uint32_t)(q.Ho * q.Wo) + (uint32_t)(oi * q.Wo + j0);
-  int a0[3], a1[3];
-  float g0[3], g1[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const bool c = j0 + t < q.Wo;
-    a0[t] = c ? (int)q.arg[o + t] : -1;
-    g0[t] = c ? q.dmp[o + t] : 0.f;
-    a1[t] = (odd && hasr && c) ? (int)q.arg[o + q.Wo + t] : -1;
-    g1[t] = (odd && hasr && c) ? q.dmp[o + q.Wo + t] : 0.f;
-  }
-  float e[4];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {   // pooled column j0 + t owns elements 2(j0+t), 2(j0+t)+1
-    if (!odd) {
-      e[2 * t] = a0[t] == 4 ? g0[t] : 0.f;
-      e[2 * t + 1] = (a0[t] == 5 ? g0[t] : 0.f) + (a0[t + 1] == 3 ? g0[t + 1] : 0.f);
-    } else {
-      e[2 * t] = (a0[t] == 7 ? g0[t] : 0.f) + (a1[t] == 1 ? g1[t] : 0.f);
-      e[2 * t + 1] = (a0[t] == 8 ? g0[t] : 0.f) + (a0[t + 1] == 6 ? g0[t + 1] : 0.f) +
-                     (a1[t] == 2 ? g1[t] : 0.f) + (a1[t + 1] == 0 ? g1[t + 1] : 0.f);
-    }
-  }
-  if (q.skip && i >= q.skip_lo && i < q.skip_hi) {
-    const float4 k = *reinterpret_cast<const float4*>(q.skip + (i - q.skip_lo));
-    e[0] += k.x; e[1] += k.y; e[2] += k.z; e[3] += k.w;
-  }
-  return make_float4(e[0], e[1], e[2], e[3]);
-}
-
-__device__ __forceinline__ float4 add_skip4(const PoolDout& q, uint32_t i, float4 g) {
+__device__ __forceinline__ float4 add_skip4(const SkipSrc& q, uint32_t i, float4 g) {
   if (i >= q.skip_lo && i < q.skip_hi) {
     const float4 k = *reinterpret_cast<const float4*>(q.skip + (i - q.skip_lo));
     g.x += k.x; g.y += k.y; g.z += k.z; g.w += k.w;
@@ -413,15 +371,14 @@ __device__ __forceinline__ float4 add_skip4(const PoolDout& q, uint32_t i, float
 // SLAB: dout formed from the dgrad conv's split-K slabs and written (see bn_stats_partial_kernel)
 // SKIP: dout + pd.skip over flat elements [pd.skip_lo, pd.skip_hi) (the decoder skip gradient,
 // added where axpy used to add it before this pass; same fp add, bit-identical)
-template <bool VEC, bool SLAB = false, bool POOL = false, bool SKIP = false>
+template <bool VEC, bool SLAB = false, bool SKIP = false>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ mgamma,
     const float* __restrict__ mbeta, int C, int HW, int N, int parts, FastDiv fdu,
     double* __restrict__ part, SlabIn sl = SlabIn{}, float* __restrict__ dout_w = nullptr,
-    PoolDout pd = PoolDout{}) {
-  static_assert(!POOL || (VEC && !SLAB), "POOL: float4 units, no slabs");
-  static_assert(!SKIP || (VEC && !SLAB && !POOL), "SKIP: float4 units of a read dout");
+    SkipSrc pd = SkipSrc{}) {
+  static_assert(!SKIP || (VEC && !SLAB), "SKIP: float4 units of a read dout");
   __shared__ double red[8];
   const int c = blockIdx.x, p = blockIdx.y;
   const int i0 = (int)((long)N * p / parts), i1 = (int)((long)N * (p + 1) / parts);
@@ -460,10 +417,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
       }
       if (VEC) {
         const long i = base + 4 * k;
-        if (POOL)
-          gv[h] = pool_dout4(pd, (uint32_t)i);
-        else if (!SLAB)
-          gv[h] = *reinterpret_cast<const float4*>(dout + i);
+        if (!SLAB) gv[h] = *reinterpret_cast<const float4*>(dout + i);
         if (SKIP) gv[h] = add_skip4(pd, (uint32_t)i, gv[h]);
         yv[h] = *reinterpret_cast<const float4*>(y + i);
         if (mask) {
@@ -527,8 +481,8 @@ __global__ void bn_bwd_final_kernel(const double* __restrict__ part, int C, int 
   dgamma[c] = (float)sgx;
 }
 
-static PoolDout skip_src(const SkipAdd& sk) {
-  PoolDout pd{};
+static SkipSrc skip_src(const SkipAdd& sk) {
+  SkipSrc pd{};
   pd.skip = sk.skip;
   pd.skip_lo = (uint32_t)sk.lo;
   pd.skip_hi = (uint32_t)sk.hi;
@@ -545,7 +499,7 @@ int bn_bwd_partial(const float* dout, const float* mask_out, const float* y, con
   MD2_CHECK_ARG(!sk.skip || (vec && sk.lo >= 0 && sk.lo <= sk.hi && sk.hi <= (long)N * C * HW),
                 "bn_bwd: skip range / HW % 4");
   if (sk.skip)
-    hipLaunchKernelGGL((bn_bwd_partial_kernel<true, false, false, true>), dim3(C, ws.parts), dim3(256), 0,
+    hipLaunchKernelGGL((bn_bwd_partial_kernel<true, false, true>), dim3(C, ws.parts), dim3(256), 0,
                        st, dout, mask_out, y, mean, invstd, mgamma, mbeta, C, (int)HW, N, ws.parts, fdu,
                        ws.partials, SlabIn{}, (float*)nullptr, skip_src(sk));
   else if (vec)
@@ -679,16 +633,15 @@ int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const
 // ---- fused finalise + backward apply: per block the channels of its planes sum the backward
 // partials in bn_bwd_final_kernel's order (bit-identical dgamma/dbeta), the owner block of each
 // channel (first unit of image 0's plane) stores dgamma[c]/dbeta[c].
-template <bool VEC, bool POOL = false, bool SKIP = false>
+template <bool VEC, bool SKIP = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const double* __restrict__ part, int parts,
     float* __restrict__ dgamma, float* __restrict__ dbeta, uint32_t nu, FastDiv fdU, FastDiv fdC,
     float invL, float* __restrict__ dy, float* __restrict__ dres, int dres_acc,
-    const float* __restrict__ mbeta, PoolDout pd = PoolDout{}) {
-  static_assert(!POOL || VEC, "POOL: float4 units");
-  static_assert(!SKIP || (VEC && !POOL), "SKIP: float4 units of a read dout");
+    const float* __restrict__ mbeta, SkipSrc pd = SkipSrc{}) {
+  static_assert(!SKIP || VEC, "SKIP: float4 units of a read dout");
   __shared__ float s_k0[256], s_db[256], s_dg[256], s_mu[256], s_is[256], s_msc[256], s_msh[256];
   const uint32_t u0 = blockIdx.x * 256u;
   const uint32_t pl0 = fdiv(u0, fdU);
@@ -731,7 +684,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
     const long i = 4L * u;
     float g[4];
     {
-      float4 t = POOL ? pool_dout4(pd, (uint32_t)i) : *reinterpret_cast<const float4*>(dout + i);
+      float4 t = *reinterpret_cast<const float4*>(dout + i);
       if (SKIP) t = add_skip4(pd, (uint32_t)i, t);
       g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
     }
@@ -784,7 +737,7 @@ int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y,
                 "bn_bwd: skip range / HW % 4");
   const float invL = 1.f / (float)((long)N * HW);
   if (sk.skip)
-    hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<true, false, true>), dim3(cdiv(n / 4, 256)), dim3(256), 0,
+    hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<true, true>), dim3(cdiv(n / 4, 256)), dim3(256), 0,
                        st, dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
                        (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy, dres, dres_accumulate, mbeta,
                        skip_src(sk));
@@ -796,42 +749,6 @@ int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y,
     hipLaunchKernelGGL(bn_bwd_apply_fused_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st,
                        dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
                        (uint32_t)n, fd(HW), fd(C), invL, dy, dres, dres_accumulate, mbeta);
-  MD2_LAUNCH_CHECK();
-  return MD2_OK;
-}
-
-// backward of the stem BN+ReLU whose output fed the 3x3/2 max pool (and, for images
-// [skip_img0, skip_img0 + skip_nimg), the decoder skip): dout = maxpool adjoint of dmp (+ skip)
-// formed inside both passes (POOL), the ReLU mask re-derived from y
-int bn_bwd_pool(const float* dmp, const unsigned char* arg, int Ho, int Wo, const float* skip,
-                int skip_img0, int skip_nimg, const float* y, const float* mean, const float* invstd,
-                const float* gamma, const float* beta, int N, int C, int H, int W, BNStatsWs ws,
-                float* dgamma, float* dbeta, float* dy, hipStream_t st) {
-  const long HW = (long)H * W;
-  MD2_TRY(check_u31((long)N * C * HW));
-  MD2_CHECK_ARG(W % 4 == 0 && Ho == (H + 1) / 2 && Wo == (W + 1) / 2, "bn_bwd_pool: W % 4, pool shape");
-  MD2_CHECK_ARG(ws.partials && ws.parts >= 1 && ws.parts <= N, "bn_bwd_pool: parts must split the images");
-  MD2_CHECK_ARG(!skip || (skip_img0 >= 0 && skip_img0 + skip_nimg <= N), "bn_bwd_pool: skip images");
-  PoolDout pd{};
-  pd.dmp = dmp;
-  pd.arg = arg;
-  pd.skip = skip;
-  pd.skip_lo = (uint32_t)((long)skip_img0 * C * HW);
-  pd.skip_hi = (uint32_t)((long)(skip_img0 + skip_nimg) * C * HW);
-  pd.Ho = Ho;
-  pd.Wo = Wo;
-  pd.fdW = fd(W);
-  pd.fdHW = fd(HW);
-  hipLaunchKernelGGL((bn_bwd_partial_kernel<true, false, true>), dim3(C, ws.parts), dim3(256), 0, st,
-                     (const float*)nullptr, (const float*)nullptr, y, mean, invstd, gamma, beta, C,
-                     (int)HW, N, ws.parts, fd(HW / 4), ws.partials, SlabIn{}, (float*)nullptr, pd);
-  MD2_LAUNCH_CHECK();
-  const long n = (long)N * C * HW;
-  const float invL = 1.f / (float)((long)N * HW);
-  hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<true, true>), dim3(cdiv(n / 4, 256)), dim3(256), 0, st,
-                     (const float*)nullptr, (const float*)nullptr, y, mean, invstd, gamma, ws.partials,
-                     ws.parts, dgamma, dbeta, (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy,
-                     (float*)nullptr, 0, beta, pd);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -880,12 +797,15 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restric
 // Gather over 2x2 input blocks: input rows {2i, 2i+1} x columns {2j, 2j+1} are touched only by
 // outputs (i..i+1, j..j+1) -- even rows/columns are tap 1 of output i, odd ones tap 2 of output
 // i and tap 0 of output i+1 -- so each thread reads 4 (arg, dy) pairs and writes 4 inputs.
-template <bool EVENW>
+// SKIP (even W): dx += skip over flat elements [sk.skip_lo, sk.skip_hi) -- the decoder skip
+// gradient on the target images, added here instead of by a separate axpy (same fp add)
+template <bool EVENW, bool SKIP = false>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ dy,
                                                           const unsigned char* __restrict__ arg,
                                                           int H, int W, int Ho, FastDiv fdWo,
                                                           FastDiv fdHo, float* __restrict__ dx,
-                                                          uint32_t n) {
+                                                          uint32_t n, SkipSrc sk = SkipSrc{}) {
+  static_assert(!SKIP || EVENW, "SKIP: even width");
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
   if (t >= n) return;
   const uint32_t r = fdiv(t, fdWo), plane = fdiv(r, fdHo);
@@ -905,10 +825,20 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
   const float e10 = (a00 == 7 ? g00 : 0.f) + (a10 == 1 ? g10 : 0.f);
   const float e11 = (a00 == 8 ? g00 : 0.f) + (a01 == 6 ? g01 : 0.f) + (a10 == 2 ? g10 : 0.f) +
                     (a11 == 0 ? g11 : 0.f);
-  float* q = dx + plane * (uint32_t)(H * W) + (2 * i) * W + 2 * j;
+  const uint32_t qi = plane * (uint32_t)(H * W) + (2 * i) * W + 2 * j;
+  float* q = dx + qi;
   if (EVENW) {
-    *reinterpret_cast<float2*>(q) = make_float2(e00, e01);
-    if (2 * i + 1 < H) *reinterpret_cast<float2*>(q + W) = make_float2(e10, e11);
+    float2 r0 = make_float2(e00, e01), r1 = make_float2(e10, e11);
+    if (SKIP && qi >= sk.skip_lo && qi < sk.skip_hi) {   // image-uniform: both rows in range
+      const float2 k0 = *reinterpret_cast<const float2*>(sk.skip + (qi - sk.skip_lo));
+      r0.x += k0.x; r0.y += k0.y;
+      if (2 * i + 1 < H) {
+        const float2 k1 = *reinterpret_cast<const float2*>(sk.skip + (qi + W - sk.skip_lo));
+        r1.x += k1.x; r1.y += k1.y;
+      }
+    }
+    *reinterpret_cast<float2*>(q) = r0;
+    if (2 * i + 1 < H) *reinterpret_cast<float2*>(q + W) = r1;
   } else {
     q[0] = e00;
     if (2 * j + 1 < W) q[1] = e01;
@@ -1006,11 +936,18 @@ int maxpool_fwd(const float* x, int N, int C, int H, int W, float* y, unsigned c
 }
 
 int maxpool_bwd(const float* dy, const unsigned char* arg, int N, int C, int H, int W, int Ho,
-                int Wo, float* dx, hipStream_t st) {
+                int Wo, float* dx, hipStream_t st, SkipAdd skip) {
   MD2_CHECK_ARG(Ho == (H + 1) / 2 && Wo == (W + 1) / 2, "maxpool_bwd: 3x3/2 pad-1 output shape");
   const long n = (long)N * C * Ho * Wo;
   MD2_TRY(check_u31((long)N * C * H * W));
-  if (W % 2 == 0)
+  MD2_CHECK_ARG(!skip.skip || (W % 2 == 0 && skip.lo >= 0 && skip.lo <= skip.hi &&
+                               skip.hi <= (long)N * C * H * W && skip.lo % ((long)H * W) == 0 &&
+                               skip.hi % ((long)H * W) == 0),
+                "maxpool_bwd: skip range (whole images, even W)");
+  if (skip.skip)
+    hipLaunchKernelGGL((maxpool_bwd_kernel<true, true>), dim3(cdiv(n, 256)), dim3(256), 0, st, dy, arg, H,
+                       W, Ho, fd(Wo), fd(Ho), dx, (uint32_t)n, skip_src(skip));
+  else if (W % 2 == 0)
     hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, arg, H,
                        W, Ho, fd(Wo), fd(Ho), dx, (uint32_t)n);
   else

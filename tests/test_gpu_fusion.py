@@ -3,9 +3,9 @@ statistics pass / the BN-backward partial pass, conv_f_bn / conv_d_bn in model.c
 split-K reduction change no bit of the train step: parameters, ADAM moments and losses after
 several steps at the benchmarked configuration (B=12, 416x128: layer3/layer4 convs run split-K)
 equal those of the separate-reduction path (MD2_FUSE_SPLITK=0).  Likewise the fused stem passes:
-BN + ReLU + max pool in one forward kernel (MD2_FUSE_POOL_FWD) and the max-pool adjoint + skip
-gradient formed inside the stem's BN-backward passes (MD2_FUSE_POOL_BWD), and the decoder skip
-gradients added inside the encoder's BN-backward passes instead of by axpy (MD2_FUSE_SKIP_BWD)."""
+BN + ReLU + max pool in one forward kernel (MD2_FUSE_POOL_FWD), the stem's decoder skip gradient
+added by the max-pool adjoint (MD2_FUSE_POOL_BWD), and the encoder stages' skip gradients added
+inside the BN-backward passes instead of by axpy (MD2_FUSE_SKIP_BWD)."""
 import os
 
 import pytest
