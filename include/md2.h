@@ -82,6 +82,10 @@ typedef struct md2_loss_out {
   signed char* vis_sel;              /* [nscales][n][h][w] argmin source (-1 = automask)      */
   float* vis_warped;                 /* [2][n][c][h][w] both sources warped by the LAST scale
                                         (train_loss vis_warped, src/training.jl:71-73)        */
+  int* vis_cell;                     /* [nscales][2][n][h][w] parity diagnostics: per pixel and
+                                        source the grid_sample bilinear cell and border state,
+                                        x | y << 12 | sx << 24 | sy << 26 (0-based cell corner;
+                                        s = 0 interior, 1 clamped to 0, 2 clamped to W-1 / H-1) */
 } md2_loss_out;
 
 /* disp[s]: [n][scale_h][scale_w]; pose: [2n][6] = (rvec, tvec) for (source s, sample i) at row
@@ -175,6 +179,11 @@ int md2_warp_photometric_fwd(const md2_warp_cfg* cfg, const float* disp, const f
 int md2_warp_photometric_bwd(const md2_warp_cfg* cfg, const float* disp, const float* Rt,
                              const float* x, const float* automask, const float* d_loss,
                              float* d_disp, float* d_Rt, void* workspace, void* stream);
+
+/* Data pipeline: N0f8 images -> Float32, out[i] = Float32(in[i]) / 255f0, the
+ * `Float32.(channelview(x))` of src/dtk.jl:45 / src/kitty.jl:58 -- batches cross PCIe as bytes.
+ * in 4-byte aligned, out 16-byte aligned. */
+int md2_unorm8_to_float(const unsigned char* in, float* out, long long n, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * 2-D convolution (Flux Conv / NNlib conv, ∇conv_data, ∇conv_filter) on gfx950 fp32 MFMA.
@@ -341,7 +350,8 @@ int md2_model_train_step_graph(md2_model* m, const float* x, const float* auto_l
  * reference has no collectives; these replace the torch.distributed plumbing so a Julia host
  * needs only this library.  RCCL is dlopen'ed on first use (MD2_ENOTSUP if absent).
  * md2_comm_get_unique_id: rank 0 creates the 128-byte id and ships it to the other ranks (file,
- * MPI, a TCP store ...); md2_comm_init then joins (collective over all ranks) on `device`.
+ * MPI, a TCP store ...); md2_comm_init then joins (collective over all ranks) on `device` (the
+ * caller's current device is restored before it returns).
  * md2_model_backward_allreduce: every backward segment on `stream`, each followed by the RCCL
  * sum of its (final) gradient range on the communicator's own stream -- bucketed, overlapped with
  * the rest of the backward; `stream` waits for all buckets before returning.  comm == NULL:
@@ -388,7 +398,9 @@ int md2_model_profile_records(md2_model* m, int max, double* ms, double* work, i
  * next call. */
 int md2_model_debug_tensor(md2_model* m, int index, const char** name, const void** ptr,
                            int* dims);
-/* eval_disparity (src/model.jl:63) on x [n][c][h][w], n <= batch; disp: per-level pointers */
+/* eval_disparity (src/model.jl:63) on x [n][c][h][w], n <= batch; disp: per-level pointers.
+ * It reuses the executor's activation buffers: a pending forward_loss is discarded and a later
+ * md2_model_backward_segment returns MD2_ESTATE until the next forward_loss. */
 int md2_model_eval_disparity(md2_model* m, const float* x, int n, const float** disp,
                              void* stream);
 

@@ -17,6 +17,7 @@ module MD2HIP
 
 using AMDGPU
 using ChainRulesCore
+import Flux
 
 const lib = get(ENV, "MD2HIP_LIB",
                 joinpath(@__DIR__, "..", "monodepth2.jl_amd", "lib", "libmd2hip.so"))
@@ -62,6 +63,7 @@ struct LossOut                                         # md2_loss_out
     loss::Ptr{Float32}; terms::Ptr{Float32}
     d_disp::NTuple{5,Ptr{Float32}}; d_pose::Ptr{Float32}
     vis_loss::Ptr{Float32}; vis_sel::Ptr{Int8}; vis_warped::Ptr{Float32}
+    vis_cell::Ptr{Int32}                               # parity diagnostics (not used here)
 end
 
 struct WarpCfg                                         # md2_warp_cfg
@@ -84,10 +86,18 @@ end
 mutable struct HIPModel
     handle::Ptr{Cvoid}
     cfg::ModelCfg
-    θ::ROCVector{Float32}
-    ∇θ::ROCVector{Float32}
-    m::ROCVector{Float32}; v::ROCVector{Float32}; step::Int
+    θ::ROCVector{Float32}          # the trainable parameters, library layout (conv taps as
+                                   # cross-correlation); Flux.params(m) == Params([m.θ])
+    ∇θ::ROCVector{Float32}         # the library's gradient buffer (same layout)
+    m::ROCVector{Float32}; v::ROCVector{Float32}; step::Int   # library ADAM state (update!)
+    packed::Bool                   # the library's packed conv weights reflect θ
 end
+
+# Flux.params(model) / gradient(θ) / Flux.Optimise.update!(opt, θ, ∇) (scripts/script.jl:84-86):
+# the one trainable array is θ.  ADAM is elementwise, so training θ in the library layout is the
+# same arithmetic as training the Flux layout; get_params / set_params! convert for checkpoints.
+Flux.@functor HIPModel (θ,)
+Flux.trainable(m::HIPModel) = (θ = m.θ,)
 
 function param_count(cfg::ModelCfg)
     ne, nel = Ref{Clonglong}(), Ref{Clonglong}()
@@ -126,9 +136,17 @@ function HIPModel(cfg::ModelCfg, θ::ROCVector{Float32})
     ∇θ = similar(θ); h = Ref{Ptr{Cvoid}}()
     check(ccall((:md2_model_create, lib), Cint,
                 (Ref{ModelCfg}, Ptr{Float32}, Ptr{Float32}, Ref{Ptr{Cvoid}}), cfg, θ, ∇θ, h))
-    m = HIPModel(h[], cfg, θ, ∇θ, fill!(similar(θ), 0), fill!(similar(θ), 0), 0)
-    check(ccall((:md2_model_repack, lib), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), m.handle, stream_ptr()))
+    m = HIPModel(h[], cfg, θ, ∇θ, fill!(similar(θ), 0), fill!(similar(θ), 0), 0, false)
+    repack!(m)
     finalizer(x -> ccall((:md2_model_destroy, lib), Cint, (Ptr{Cvoid},), x.handle), m)
+end
+
+# after the caller changed m.θ in place (Flux.Optimise.update!, loading a checkpoint): re-pack the
+# library's conv weights.  train_loss does it by itself after every pullback (see below).
+function repack!(m::HIPModel)
+    check(ccall((:md2_model_repack, lib), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), m.handle, stream_ptr()))
+    m.packed = true
+    return m
 end
 
 # (m)(x, source_ids, target_id) -- disparities (Julia (w,h,1,n) views of library memory) and
@@ -157,17 +175,32 @@ end
 """
     train_loss(m, x, auto_loss, cache, params, do_visualization=false)
 
-`train_loss` of src/training.jl:21-78 on the HIP path: returns `(loss, vis_disparity, vis_warped,
-vis_loss)` like the reference (`nothing`s when `do_visualization` is false).  The forward also
-runs the fused loss-tail pullback; the rrule below finishes the backward.
+`train_loss` of src/training.jl:21-78 on the HIP path, with the reference's return convention:
+`(loss, vis_disparity, vis_warped, vis_loss)` where `loss` is a host `Float32` scalar
+(`loss / T(length(cache.scales))`, :77) and the visualisation outputs are host arrays
+(`cpu(disparities[end])` (W,H,1,n), `cpu.(warped_images)` two (W,H,C,n), `cpu(warp_loss)`
+(W,H,1,n); `nothing`s when `do_visualization` is false, :34-37,71-74).  The forward also runs the
+fused loss-tail pullback; the rrule finishes the backward.  `cache` / `params` are the ones the
+model was built with (md2_model_cfg); the arguments are kept for the reference's signature.
+
+Zygote: `gradient(() -> train_loss(m, x, ...)[1], Flux.params(m))` (the implicit-parameter loop
+of scripts/script.jl:84-86, src/simple_depth.jl:25-42) returns the gradient under `m.θ`, in
+m.θ's own layout, so `Flux.Optimise.update!(opt, Flux.params(m), ∇)` updates m.θ consistently.
 """
-function train_loss(m::HIPModel, x::ROCArray{Float32,5}, auto_loss, cache, params,
-                    do_visualization::Bool=false)
+train_loss(m::HIPModel, x::ROCArray{Float32,5}, auto_loss, cache, params,
+           do_visualization::Bool=false) =
+    _train_loss(m, m.θ, x, auto_loss, do_visualization)     # m.θ read in traced code: accum_param
+
+function _train_loss(m::HIPModel, θ::ROCVector{Float32}, x::ROCArray{Float32,5}, auto_loss,
+                     do_visualization::Bool)
+    θ === m.θ || error("train_loss: θ must be the model's own parameter vector")
+    m.packed || repack!(m)               # θ may have been updated in place since the last step
     loss = ROCVector{Float32}(undef, 1)
     check(ccall((:md2_model_forward_loss, lib), Cint,
                 (Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
                 m.handle, x, ptr(auto_loss), loss, C_NULL, stream_ptr()))
-    do_visualization || return (loss, nothing, nothing, nothing)
+    l = Array(loss)[1]                   # host scalar, as the reference's mean(...) / T(...)
+    do_visualization || return (l, nothing, nothing, nothing)
     disps, pose = outputs(m)
     cfg = loss_cfg(m); n = m.cfg.batch; c = m.cfg.in_channels; W = m.cfg.width; H = m.cfg.height
     vis_loss = ROCArray{Float32}(undef, W, H, n, cfg.nscales)
@@ -176,15 +209,15 @@ function train_loss(m::HIPModel, x::ROCArray{Float32,5}, auto_loss, cache, param
     tmp = ROCVector{Float32}(undef, 1)
     ws = ROCVector{UInt8}(undef, ccall((:md2_loss_workspace_size, lib), Csize_t, (Ref{LossCfg},), cfg))
     out = LossOut(pointer(tmp), C_NULL, ntuple(_ -> Ptr{Float32}(C_NULL), 5), C_NULL,
-                  pointer(vis_loss), pointer(vis_sel), pointer(vis_warped))
+                  pointer(vis_loss), pointer(vis_sel), pointer(vis_warped), C_NULL)
     dptrs = [pointer(d) for d in disps]
     check(ccall((:md2_loss_fwd_bwd, lib), Cint,
                 (Ref{LossCfg}, Ptr{Ptr{Float32}}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Cfloat,
                  Ref{LossOut}, Ptr{UInt8}, Ptr{Cvoid}),
                 cfg, dptrs, pose, x, ptr(auto_loss), 1f0, out, ws, stream_ptr()))
     # training.jl:34-37,71-74: last disparity, both warped sources and the last scale's loss map
-    return (loss, disps[end], (vis_warped[:, :, :, :, 1], vis_warped[:, :, :, :, 2]),
-            reshape(vis_loss[:, :, :, end], W, H, 1, n))
+    return (l, Array(disps[end]), (Array(vis_warped[:, :, :, :, 1]), Array(vis_warped[:, :, :, :, 2])),
+            Array(reshape(vis_loss[:, :, :, end], W, H, 1, n)))
 end
 
 # gradient(θ) do train_loss(...)[1] end: the remaining backward segments -> m.∇θ.  `bucket(off,
@@ -202,29 +235,40 @@ function gradient!(m::HIPModel; bucket=(off, len) -> nothing)
 end
 
 # Zygote: d(train_loss(...)[1])/dθ.  The loss cotangent enters the library's backward itself
-# (md2_model_loss_cotangent scales the fused loss tail's d disp / d pose before segment 0); the
-# returned tangent is in Flux layout (md2_model_get_grads: conv kernels as true convolutions).
-function ChainRulesCore.rrule(::typeof(train_loss), m::HIPModel, x, auto_loss, cache, params,
-                              do_visualization::Bool=false)
-    y = train_loss(m, x, auto_loss, cache, params, do_visualization)
+# (md2_model_loss_cotangent scales the fused loss tail's d disp / d pose before segment 0).  The
+# θ tangent is a fresh array in θ's own (library) layout -- what Flux.Optimise.update! adds to
+# θ; the Flux-layout gradient (true-convolution kernels) is flux_gradient(m).  The caller is
+# expected to update θ next, so the packed weights are marked stale (re-packed by the next
+# train_loss, or already by the library's own update!).
+function ChainRulesCore.rrule(::typeof(_train_loss), m::HIPModel, θ::ROCVector{Float32}, x, auto_loss,
+                              do_visualization::Bool)
+    y = _train_loss(m, θ, x, auto_loss, do_visualization)
     function train_loss_pullback(Δ)
-        Δl = Δ[1] isa AbstractZero ? 0f0 : Float32(sum(Array(unthunk(Δ[1]))))
+        Δl = unthunk(Δ[1])
+        Δl = Δl isa AbstractZero ? 0f0 : Float32(Δl)
         check(ccall((:md2_model_loss_cotangent, lib), Cint, (Ptr{Cvoid}, Cfloat, Ptr{Cvoid}),
                     m.handle, Δl, stream_ptr()))
         gradient!(m)
-        ∇flux = similar(m.∇θ)
-        check(ccall((:md2_model_get_grads, lib), Cint, (Ptr{Cvoid}, Ptr{Float32}, Ptr{Cvoid}),
-                    m.handle, ∇flux, stream_ptr()))
-        return (NoTangent(), Tangent{HIPModel}(; θ=∇flux), NoTangent(), NoTangent(), NoTangent(),
-                NoTangent(), NoTangent())
+        m.packed = false
+        return (NoTangent(), NoTangent(), copy(m.∇θ), NoTangent(), NoTangent(), NoTangent())
     end
     return y, train_loss_pullback
+end
+
+# the last gradient in Flux layout (Flux.params order, conv kernels as true convolutions): what
+# Zygote returns for a Flux Model's params -- for comparing against / exporting to the reference
+function flux_gradient(m::HIPModel)
+    ∇flux = similar(m.∇θ)
+    check(ccall((:md2_model_get_grads, lib), Cint, (Ptr{Cvoid}, Ptr{Float32}, Ptr{Cvoid}),
+                m.handle, ∇flux, stream_ptr()))
+    return ∇flux
 end
 
 # Flux-layout parameters in / out of the model (device copies with the conv taps flipped)
 function set_params!(m::HIPModel, flux::ROCVector{Float32})
     check(ccall((:md2_model_set_params, lib), Cint, (Ptr{Cvoid}, Ptr{Float32}, Ptr{Cvoid}),
                 m.handle, flux, stream_ptr()))
+    m.packed = true                      # md2_model_set_params re-packs
     return m
 end
 function get_params(m::HIPModel)
@@ -240,6 +284,8 @@ function update!(m::HIPModel, η; β=(0.9f0, 0.999f0), ϵ=1f-8, grad_scale=1f0)
     check(ccall((:md2_model_adam, lib), Cint,
                 (Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}, Cfloat, Cfloat, Cfloat, Cfloat, Cint, Cfloat, Ptr{Cvoid}),
                 m.handle, m.m, m.v, η, β[1], β[2], ϵ, m.step, grad_scale, stream_ptr()))
+    m.packed = true                      # md2_model_adam re-packs
+    return m
 end
 
 # eval_disparity(m, x) -- src/model.jl:63; x::(W,H,C,n), n <= batch
@@ -447,6 +493,7 @@ end
 # One whole step (forward, loss, backward, ADAM(η) with β = (0.9, 0.999), ϵ = 1e-8) replayed as a
 # captured hipGraph; the same kernels in the same order as train_loss + gradient! + update!
 function train_step_graph!(m::HIPModel, x::ROCArray{Float32,5}, auto_loss, η)
+    m.packed || repack!(m)
     m.step += 1; loss = ROCVector{Float32}(undef, 1)
     check(ccall((:md2_model_train_step_graph, lib), Cint,
                 (Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Cfloat, Cint,
@@ -520,16 +567,29 @@ end
 
 # ------------------------------------------------------------------------------------------------
 # Data parallel: one Julia process per GPU over the library's own RCCL communicator (SURVEY 8e;
-# the reference's loop is scripts/script.jl:84-86).  Rank 0 writes the unique id to `idfile`.
+# the reference's loop is scripts/script.jl:84-86).  Rank 0 writes the unique id to `idfile`,
+# tagged with `run_id` -- a string unique to this launch that every rank gets from the launcher
+# (e.g. the job id) -- and the other ranks accept only a file carrying their own tag, so a file
+# left over from an earlier run can never hand them a stale id (ncclCommInitRank would hang).
 # ------------------------------------------------------------------------------------------------
-function comm_init(rank, nranks, device, idfile)
+function comm_init(rank, nranks, device, idfile; run_id=get(ENV, "MD2_RUN_ID", ""))
+    isempty(run_id) && error("comm_init: pass run_id (or set MD2_RUN_ID) unique to this launch")
+    tag = Vector{UInt8}(run_id)
     id = zeros(UInt8, 128)
     if rank == 0
         check(ccall((:md2_comm_get_unique_id, lib), Cint, (Ptr{UInt8},), id))
-        write(idfile * ".tmp", id); mv(idfile * ".tmp", idfile; force=true)
+        write(idfile * ".tmp", vcat(id, tag)); mv(idfile * ".tmp", idfile; force=true)
     else
-        while !isfile(idfile); sleep(0.05); end
-        id .= read(idfile)
+        while true
+            if isfile(idfile)
+                b = read(idfile)
+                if length(b) == 128 + length(tag) && b[129:end] == tag
+                    id .= b[1:128]
+                    break
+                end
+            end
+            sleep(0.05)
+        end
     end
     c = Ref{Ptr{Cvoid}}()
     check(ccall((:md2_comm_init, lib), Cint, (Cint, Cint, Ptr{UInt8}, Cint, Ref{Ptr{Cvoid}}),
@@ -539,6 +599,7 @@ end
 
 # forward + loss + backward with each bucket's RCCL all-reduce overlapped + ADAM (1/nranks)
 function train_step_dp!(m::HIPModel, comm::Ptr{Cvoid}, x, auto_loss, η; β=(0.9f0, 0.999f0), ϵ=1f-8)
+    m.packed || repack!(m)
     m.step += 1; loss = ROCVector{Float32}(undef, 1)
     check(ccall((:md2_model_train_step_dp, lib), Cint,
                 (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32},

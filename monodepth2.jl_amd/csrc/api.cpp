@@ -2,6 +2,7 @@
 #include "../../include/md2.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -49,6 +50,18 @@ static LossTailCfg to_tail_cfg(const md2_loss_cfg* c) {
 
 using namespace md2;
 
+namespace md2 {
+int tuning_knob(const char* name, int dflt) {
+  static const bool on = [] {
+    const char* t = std::getenv("MD2_TUNING");
+    return t && std::atoi(t) == 1;
+  }();
+  if (!on) return dflt;
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+}  // namespace md2
+
 extern "C" {
 
 int md2_abi_version(void) { return MD2_ABI_VERSION; }
@@ -84,6 +97,7 @@ int md2_loss_fwd_bwd(const md2_loss_cfg* cfg, const float* const* disp, const fl
   o.vis_loss = out->vis_loss;
   o.vis_sel = out->vis_sel;
   o.vis_warped = out->vis_warped;
+  o.vis_cell = out->vis_cell;
   return loss_tail_run(to_tail_cfg(cfg), disp, pose, x, automask, dloss, o, workspace,
                        (hipStream_t)stream);
 }

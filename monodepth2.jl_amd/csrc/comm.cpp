@@ -4,13 +4,15 @@
 //
 // RCCL is bound at run time (dlopen of librccl.so.1, RTLD_LOCAL): the library has no link-time
 // dependency on it, and in a process that already loaded RCCL (PyTorch) the loaded copy is
-// reused.  One communicator = one rank on one device + its own non-blocking comm stream.  The
+// reused.  MD2_RCCL_LIB names another library exporting the same five nccl* symbols (the tests'
+// call-recording stub); it is tried first.  One communicator = one rank on one device + its own non-blocking comm stream.  The
 // backward runs on the caller's stream; after segment k is enqueued an event orders the RCCL sum
 // of that segment's (now final) gradient range on the comm stream, so the all-reduce of the
 // decoder / deep encoder stages overlaps the remaining backward; the caller's stream then waits
 // for every bucket before ADAM applies 1/nranks.
 #include <dlfcn.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -36,9 +38,10 @@ int rccl(Rccl** out) {
   static bool tried = false;
   if (!tried) {
     tried = true;
-    const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+    const char* over = std::getenv("MD2_RCCL_LIB");
+    const char* names[] = {over, "librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
     for (const char* n : names)
-      if ((r.h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+      if (n && *n && (r.h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
     if (r.h) {
       r.get_unique_id = (decltype(r.get_unique_id))dlsym(r.h, "ncclGetUniqueId");
       r.init_rank = (decltype(r.init_rank))dlsym(r.h, "ncclCommInitRank");
@@ -94,7 +97,15 @@ int md2_comm_init(int rank, int nranks, const char* id, int device, md2_comm** o
   MD2_CHECK_ARG(out && id && nranks >= 1 && rank >= 0 && rank < nranks && device >= 0, "comm_init args");
   Rccl* r;
   MD2_TRY(rccl(&r));
+  // RCCL binds the communicator and the comm stream to the CURRENT device: switch to `device`
+  // for the setup and give the caller its own current device back on every path
+  int prev = 0;
+  MD2_HIP(hipGetDevice(&prev));
   MD2_HIP(hipSetDevice(device));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{prev};
   md2_comm* c = new md2_comm();
   c->r = r;
   c->rank = rank;

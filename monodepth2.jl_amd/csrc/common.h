@@ -45,6 +45,12 @@ const char* last_error();
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Kernel / planner tuning knobs (tools/*_sweep.sh, tools/ab_*.sh): MD2_<name>=<int> is honoured
+// ONLY when MD2_TUNING=1 is also set; otherwise every knob is its measured default and the
+// library's kernels and plans do not depend on the environment.  (The fusion switches
+// MD2_FUSE_* are separate: each is tested for bit-identity, tests/test_gpu_fusion.py.)
+int tuning_knob(const char* name, int dflt);
+
 // ---------------------------------------------------------------------------------------------
 // device helpers
 // ---------------------------------------------------------------------------------------------
@@ -147,6 +153,25 @@ __device__ __forceinline__ void block_sum256(float (&v)[NV], float* red) {
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = red[i] + red[NV + i] + red[2 * NV + i] + red[3 * NV + i];
+  }
+  __syncthreads();
+}
+
+// the same in fp64 (shuffle tree; `red` holds 4*NV doubles): the cancelling global sums of the
+// loss tail (disparity means, the smoothness normalisation constant)
+template <int NV>
+__device__ __forceinline__ void block_sum256_d(double (&v)[NV], double* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum_d(v[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[wid * NV + i] = v[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = (red[i] + red[NV + i]) + (red[2 * NV + i] + red[3 * NV + i]);
   }
   __syncthreads();
 }

@@ -522,10 +522,7 @@ long strip_units(const ConvShape& s, int R) { return (long)s.N * cdiv(s.H, R) * 
 
 // strip path for the wide heads; MD2_HEAD_STRIP=0 keeps the pixel-per-lane kernels
 bool strip_ok(const ConvShape& s) {
-  static const int on = [] {
-    const char* e = getenv("MD2_HEAD_STRIP");
-    return e ? atoi(e) : 1;
-  }();
+  static const int on = tuning_knob("MD2_HEAD_STRIP", 1);
   return on && s.W >= 64 && s.H >= 4;
 }
 // forward / filter gradient strips only where they give enough blocks (measured: head5, head4;

@@ -26,7 +26,13 @@ struct PhotoScale {
   float* partials;        // [N*tiles][25]: loss sum, dR0(9) dt0(3), dR1(9) dt1(3)
   float* loss_map;        // [N][H][W] per-pixel warp loss (train_loss vis_loss) or nullptr
   signed char* sel_map;   // [N][H][W] chosen source (0/1, -1 = automask) or nullptr
+  int* cell_map;          // [2][N][H][W] bilinear cell + border flags per source (parity
+                          // diagnostics, PHOTO_CELL_* packing) or nullptr
 };
+
+// cell_map packing: x cell (bits 0-11), y cell (12-23), x border state (24-25), y (26-27);
+// state 0 = interior (coordinate differentiable), 1 = clamped to 0, 2 = clamped to W-1 / H-1
+constexpr int PHOTO_CELL_YSHIFT = 12, PHOTO_CELL_FXSHIFT = 24, PHOTO_CELL_FYSHIFT = 26;
 
 struct PhotoArgs {
   PhotoScale sc[MAX_SCALES];
@@ -56,11 +62,12 @@ struct SmoothArgs {
   float rx, ry;
   const float* img;          // target frame of sample 0 ([C][H][W])
   long img_sample_stride;
-  const float* mean_partials;  // [N][mean_parts] sums of the upsampled disparity
+  const double* mean_partials;  // [N][mean_parts] sums of the upsampled disparity (fp64)
   int mean_parts;
   float ws;                  // d(total)/d(smooth term) = smoothness * scale / nscales * upstream
   float* g_disp;             // [N][H][W] accumulated
-  float* partials;           // [blocks][2]: smooth loss sum, sum(u * d)
+  float* partials;           // [blocks][2]: smooth loss sum, sum(u * d) (fp32)
+  double* tsum;              // [blocks] sum(u * d) in fp64 (the normalisation constant) or nullptr
   int N, W, H;
 };
 
@@ -73,9 +80,9 @@ struct UpAdjArgs {
   const float* disp;         // [N][dh][dw] sigmoid output (for the derivative)
   int dw, dh;
   float rx, ry;
-  const float* mean_partials;
+  const double* mean_partials;
   int mean_parts;
-  const float* smooth_partials;  // [N][smooth_parts][2] or nullptr
+  const double* smooth_tsum;     // [N][smooth_parts] fp64 sum(u * d) or nullptr
   int smooth_parts;
   float ws;
   int sigmoid;               // multiply by s(1-s)
@@ -93,7 +100,7 @@ struct DispSumArgs {
   const float* disp;         // [N][dh][dw]
   int dw, dh;
   float rx, ry;
-  float* out;                // [N][parts]
+  double* out;               // [N][parts] (fp64: the mean feeds a cancelling normalisation)
 };
 struct DispSumBatch {
   DispSumArgs s[MAX_SCALES];

@@ -73,19 +73,19 @@ __device__ __forceinline__ void ray_at(const Geom& g, int gx, int gy, float& r0,
 // ---------------------------------------------------------------------------------------------
 // all scales in one launch: grid (parts, N, nscales)
 __global__ __launch_bounds__(256) void disp_sum_kernel(DispSumBatch b) {
-  __shared__ float red[4];
+  __shared__ double red[4];
   const int n = blockIdx.y;
   const DispSumArgs a = b.s[blockIdx.z];
   const int W = b.W, H = b.H, parts = b.parts;
   const long P = (long)W * H;
   const float* d = a.disp + (long)n * a.dw * a.dh;
-  float s = 0.f;
+  double s = 0.0;
   for (long q = (long)blockIdx.x * 256 + threadIdx.x; q < P; q += (long)parts * 256) {
     const int X = (int)(q % W), Y = (int)(q / W);
-    s += disp_at(d, a.dw, a.dh, a.rx, a.ry, W, H, X, Y);
+    s += (double)disp_at(d, a.dw, a.dh, a.rx, a.ry, W, H, X, Y);
   }
-  float v[1] = {s};
-  block_sum256<1>(v, red);
+  double v[1] = {s};
+  block_sum256_d<1>(v, red);
   if (threadIdx.x == 0) a.out[n * parts + blockIdx.x] = v[0];
 }
 
@@ -100,6 +100,7 @@ __global__ __launch_bounds__(256) void smooth_kernel(SmoothBatch b) {
   constexpr int EW = SM_W + 1, EH = SM_H + 1, NE = EW * EH;
   __shared__ float s_ex[NE], s_ey[NE];
   __shared__ float s_red[4 * 3];
+  __shared__ double s_redd[4];
   const int sc = blockIdx.z / b.s[0].N;       // scale; every scale shares N, W, H
   const SmoothArgs a = b.s[sc];
   const int W = a.W, H = a.H;
@@ -110,10 +111,9 @@ __global__ __launch_bounds__(256) void smooth_kernel(SmoothBatch b) {
   const float* img = a.img + (long)n * a.img_sample_stride;
   float inv = 1.f;                          // slow_depth: no mean normalisation
   if (a.mean_partials) {
-    float m = 0.f;
+    double m = 0.0;
     for (int k = 0; k < a.mean_parts; ++k) m += a.mean_partials[n * a.mean_parts + k];
-    m = m / (float)HW;
-    inv = 1.f / (m + 1e-7f);
+    inv = 1.f / ((float)(m / (double)HW) + 1e-7f);
   }
   const float cx = 1.f / ((float)a.N * (float)H * (float)(W - 1));
   const float cy = 1.f / ((float)a.N * (float)(H - 1) * (float)W);
@@ -155,6 +155,7 @@ __global__ __launch_bounds__(256) void smooth_kernel(SmoothBatch b) {
   }
   __syncthreads();
   float tsum = 0.f;
+  double tsumd = 0.0;
   for (int i = threadIdx.x; i < SM_W * SM_H; i += 256) {
     const int tx = i % SM_W, ty = i / SM_W;
     const int gx = x0 + tx, gy = y0 + ty;
@@ -163,14 +164,21 @@ __global__ __launch_bounds__(256) void smooth_kernel(SmoothBatch b) {
     const float u = s_ex[e] - s_ex[e - 1] + s_ey[e] - s_ey[e - EW];
     const long q = ((long)n * H + gy) * W + gx;
     a.g_disp[q] += a.ws * u * inv;
-    tsum += u * disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy);
+    const float dv = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy);
+    tsum += u * dv;
+    tsumd += (double)u * (double)dv;
   }
   float v[3] = {lx + ly, tsum, 0.f};
   block_sum256<3>(v, s_red);
+  const long blk = ((long)n * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
   if (threadIdx.x == 0) {
-    const long blk = ((long)n * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     a.partials[blk * 2 + 0] = v[0];
     a.partials[blk * 2 + 1] = v[1];
+  }
+  if (a.tsum) {                               // block-uniform
+    double t[1] = {tsumd};
+    block_sum256_d<1>(t, s_redd);
+    if (threadIdx.x == 0) a.tsum[blk] = t[0];
   }
 }
 
@@ -203,19 +211,21 @@ __device__ __forceinline__ float up_weight(int X, int j, int in, float r) {
 // All scales in one launch: grid (max dh, N, nscales); rows past a scale's dh exit at once.
 __global__ __launch_bounds__(256) void up_adjoint_kernel(UpAdjBatch b) {
   extern __shared__ float s_col[];           // [W]
-  __shared__ float s_red[2][4];
+  __shared__ double s_red[2][4];
   const UpAdjArgs a = b.s[blockIdx.z];
   const int W = a.W, H = a.H;
   const int i = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
   if (i >= a.dh) return;                     // block-uniform, before any barrier
   float cn = 0.f;
-  if (a.smooth_partials) {
-    float m = 0.f, T = 0.f;
+  if (a.smooth_tsum) {
+    // the mean-normalisation constant -ws * sum(u d) / (m^2 W H): sum(u d) is a near-cancelling
+    // sum (the normalised disparity is scale invariant, so its gradient is orthogonal to d), so
+    // both sums are formed in fp64 from fp64 partials
+    double m = 0.0, T = 0.0;
     for (int k = tid; k < a.mean_parts; k += 256) m += a.mean_partials[n * a.mean_parts + k];
-    for (int k = tid; k < a.smooth_parts; k += 256)
-      T += a.smooth_partials[((long)n * a.smooth_parts + k) * 2 + 1];
-    m = wave_sum(m);
-    T = wave_sum(T);
+    for (int k = tid; k < a.smooth_parts; k += 256) T += a.smooth_tsum[(long)n * a.smooth_parts + k];
+    m = wave_sum_d(m);
+    T = wave_sum_d(T);
     if ((tid & 63) == 0) {
       s_red[0][tid >> 6] = m;
       s_red[1][tid >> 6] = T;
@@ -223,9 +233,9 @@ __global__ __launch_bounds__(256) void up_adjoint_kernel(UpAdjBatch b) {
     __syncthreads();
     m = (s_red[0][0] + s_red[0][1]) + (s_red[0][2] + s_red[0][3]);
     T = (s_red[1][0] + s_red[1][1]) + (s_red[1][2] + s_red[1][3]);
-    m = m / ((float)W * (float)H);
-    const float mi = 1.f / (m + 1e-7f);
-    cn = -a.ws * T * mi * mi / ((float)W * (float)H);
+    const double WH = (double)W * (double)H;
+    const double mi = 1.0 / ((double)(float)(m / WH) + 1e-7);
+    cn = (float)(-(double)a.ws * T * mi * mi / WH);
   }
   const float* g = a.g_full + (long)n * W * H;
   const long orow = ((long)n * a.dh + i) * a.dw;

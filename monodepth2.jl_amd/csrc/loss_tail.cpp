@@ -9,7 +9,8 @@ namespace {
 inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
 struct TailLayout {
-  size_t Rt, dRt, g_full[MAX_SCALES], mean, photo[MAX_SCALES], smooth[MAX_SCALES], terms, total;
+  size_t Rt, dRt, g_full[MAX_SCALES], mean, photo[MAX_SCALES], smooth[MAX_SCALES], tsum[MAX_SCALES],
+      terms, total;
 };
 
 TailLayout layout(const LossTailCfg& c) {
@@ -22,11 +23,12 @@ TailLayout layout(const LossTailCfg& c) {
   };
   L.Rt = take(sizeof(float) * 2 * c.N * 12);
   L.dRt = take(sizeof(float) * 2 * c.N * 12);
-  L.mean = take(sizeof(float) * (size_t)c.nscales * c.N * MEAN_PARTS);
+  L.mean = take(sizeof(double) * (size_t)c.nscales * c.N * MEAN_PARTS);
   for (int s = 0; s < c.nscales; ++s) {
     L.g_full[s] = take(sizeof(float) * (size_t)c.N * c.W * c.H);
     L.photo[s] = take(sizeof(float) * 25 * photometric_blocks(c.W, c.H, c.N, c.nscales));
     L.smooth[s] = take(sizeof(float) * 2 * smooth_blocks(c.W, c.H, c.N));
+    L.tsum[s] = take(sizeof(double) * smooth_blocks(c.W, c.H, c.N));
   }
   L.terms = take(sizeof(float) * 2 * MAX_SCALES);
   L.total = off;
@@ -54,7 +56,7 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
   char* ws = (char*)workspace;
   float* Rt = (float*)(ws + L.Rt);
   float* dRt = (float*)(ws + L.dRt);
-  float* mean = (float*)(ws + L.mean);
+  double* mean = (double*)(ws + L.mean);
   float* tterms = terms ? terms : (float*)(ws + L.terms);
 
   Geom g;
@@ -110,6 +112,7 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     ps.partials = (float*)(ws + L.photo[s]);
     ps.loss_map = o.vis_loss ? o.vis_loss + s * plane : nullptr;
     ps.sel_map = o.vis_sel ? o.vis_sel + s * plane : nullptr;
+    ps.cell_map = o.vis_cell ? o.vis_cell + 2 * s * plane : nullptr;
     db.s[s] = DispSumArgs{disp[s], c.dw[s], c.dh[s], ps.rx, ps.ry, mean + (size_t)s * c.N * MEAN_PARTS};
   }
   MD2_TRY(launch_disp_sum(db, c.nscales, st));   // every scale's mean in one launch
@@ -124,8 +127,9 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
   int nua = 0;
   for (int s = 0; s < c.nscales; ++s) {
     const PhotoScale& ps = pa.sc[s];
-    float* mp = mean + (size_t)s * c.N * MEAN_PARTS;
+    double* mp = mean + (size_t)s * c.N * MEAN_PARTS;
     float* sp = (float*)(ws + L.smooth[s]);
+    double* tp = (double*)(ws + L.tsum[s]);
     SmoothArgs& sa = sas[s];
     sa = SmoothArgs{};
     sa.disp = disp[s];
@@ -140,6 +144,7 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     sa.ws = up * c.smooth_w[s];
     sa.g_disp = ps.g_disp;
     sa.partials = sp;
+    sa.tsum = c.smooth_normalize ? tp : nullptr;
     sa.N = c.N;
     sa.W = c.W;
     sa.H = c.H;
@@ -153,7 +158,7 @@ int loss_tail_run(const LossTailCfg& c, const float* const* disp, const float* p
     ua.ry = ps.ry;
     ua.mean_partials = mp;
     ua.mean_parts = MEAN_PARTS;
-    ua.smooth_partials = c.smooth_normalize ? sp : nullptr;
+    ua.smooth_tsum = c.smooth_normalize ? tp : nullptr;
     ua.smooth_parts = (int)(smooth_blk / c.N);
     ua.ws = sa.ws;
     ua.sigmoid = c.sigmoid_grad;

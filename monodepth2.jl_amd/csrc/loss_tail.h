@@ -32,6 +32,7 @@ struct LossTailOut {
   float* vis_loss;
   signed char* vis_sel;
   float* vis_warped;                    // [2][N][C][H][W] warped sources at the last scale or nullptr
+  int* vis_cell;                        // [nscales][2][N][H][W] bilinear cells (diagnostics) or nullptr
   hipEvent_t* photo_events = nullptr;   // optional [2]: around the (all-scale) photometric launch
 };
 

@@ -1252,7 +1252,11 @@ int model_train_step_graph(Model* m, const float* x, const float* auto_loss, flo
 
 
 int model_backward_segment(Model* m, int k, long* off, long* len, hipStream_t st) {
-  MD2_CHECK_ARG(m && m->cur_x, "backward before forward");
+  MD2_CHECK_ARG(m, "model");
+  if (!m->cur_x) {
+    set_error("backward_segment: no pending forward_loss (none yet, or eval_disparity ran since)");
+    return MD2_ESTATE;
+  }
   MD2_CHECK_ARG(k >= 0 && k < 6, "segment index");
   long b = 0, e = 0;
   const ArchSpec& S = m->spec;
@@ -1363,6 +1367,9 @@ int model_features(Model* m, const float** feat, int* c, int* h, int* w) {
 
 int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipStream_t st) {
   MD2_CHECK_ARG(m && x && n >= 1 && n <= m->N, "eval_disparity: 1 <= n <= batch");
+  // inference reuses the executor's activation buffers: a pending train forward is gone, and a
+  // backward after this must fail instead of differentiating the eval batch
+  m->cur_x = nullptr;
   TensorIn in = Model::tin(x, m->cfg.arch.in_ch, (long)m->cfg.H * m->cfg.W);
   MD2_TRY(m->encoder_fwd(in, n, st));
   MD2_TRY(m->decoder_fwd(n, 0, st));

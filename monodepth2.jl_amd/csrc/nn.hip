@@ -1145,10 +1145,7 @@ int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStrea
 int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStream_t st) {
   const long n = (long)N * C * h * w;
   MD2_TRY(check_u31(4 * n));
-  static const int tiled = [] {
-    const char* e = getenv("MD2_UP_TILED");
-    return e ? atoi(e) : 1;
-  }();
+  static const int tiled = tuning_knob("MD2_UP_TILED", 1);
   if (tiled && (long)N * C <= 65535)
     hipLaunchKernelGGL(upsample2_bwd_tile_kernel, dim3(cdiv(w, UPB_TW), cdiv(h, UPB_TH), N * C),
                        dim3(256), 0, st, dy, h, w, up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx);

@@ -81,6 +81,26 @@ __device__ __forceinline__ void window_idx(int gx, int gy, int W, int H, int x0,
 // ---------------------------------------------------------------------------------------------
 // automasking_loss: min over sources of 0.85 mean_c SSIM(src, tgt) + 0.15 mean_c |tgt - src|
 // ---------------------------------------------------------------------------------------------
+// N0f8 pixels -> Float32 (the data pipeline's `Float32.(channelview(x))`, src/dtk.jl:45,
+// src/kitty.jl:58): one byte in, Float32(u) / 255f0 out, 16 bytes per lane per trip.
+__global__ __launch_bounds__(256) void unorm8_kernel(const uint8_t* __restrict__ in, long n,
+                                                     float* __restrict__ out) {
+  const long stride = (long)gridDim.x * 256 * 4;
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 4 <= n) {
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(in + i);
+      float4 f;
+      f.x = (float)(v & 0xff) / 255.f;
+      f.y = (float)((v >> 8) & 0xff) / 255.f;
+      f.z = (float)((v >> 16) & 0xff) / 255.f;
+      f.w = (float)(v >> 24) / 255.f;
+      *reinterpret_cast<float4*>(out + i) = f;
+    } else {
+      for (long k = i; k < n; ++k) out[k] = (float)in[k] / 255.f;
+    }
+  }
+}
+
 template <int C>
 __global__ __launch_bounds__(256) void automask_kernel(const float* __restrict__ x, long x_ss,
                                                        long x_fs, int target, int src0, int src1,
@@ -580,6 +600,18 @@ int md2_grid_sample_border_bwd(const float* x, const float* grid, const float* d
 
 // smooth_loss(disparity [n][h][w], image [n][c][h][w]) -- the smoothness kernel of the loss tail
 // on a full-resolution disparity, no mean normalisation, upstream weight dloss.
+int md2_unorm8_to_float(const unsigned char* in, float* out, long long n, void* stream) {
+  MD2_CHECK_ARG(in && out && n >= 0, "unorm8_to_float args");
+  MD2_CHECK_ARG(((uintptr_t)in & 3) == 0 && ((uintptr_t)out & 15) == 0,
+                "unorm8_to_float: in must be 4-byte and out 16-byte aligned");
+  if (n == 0) return MD2_OK;
+  const long blocks = std::min<long>(4096, cdiv(n, 256 * 4));
+  hipLaunchKernelGGL(unorm8_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)in, (long)n, out);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 size_t md2_smooth_loss_workspace_size(int n, int w, int h) {
   return a256(sizeof(float) * (size_t)n * w * h) + a256(sizeof(float) * 2 * smooth_blocks(w, h, n));
 }

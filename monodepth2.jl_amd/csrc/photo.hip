@@ -77,7 +77,10 @@ using Slot = std::integral_constant<int, N_>;
 
 }  // namespace
 
-template <int C>
+// CELLS: also record each owned pixel's bilinear cell / border state (sc.cell_map, parity
+// diagnostics).  A separate instantiation so the production kernel's registers are untouched;
+// the arithmetic is the same source, so values and decisions are the same.
+template <int C, bool CELLS>
 __global__ __launch_bounds__(64) MD2_PHOTO_WPE
 void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
   constexpr int NF = 6 * C;       // coefficients per pixel: per source and channel A, B, Cc
@@ -253,6 +256,11 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
       bfy[sp] = yc - (float)yi;
       bmx[sp] = (ix > 0.f && ix < Wm1) ? 1.f : 0.f;   // clamp gradient masks
       bmy[sp] = (iy > 0.f && iy < Hm1) ? 1.f : 0.f;
+      if (CELLS && outl && R >= y0 && R < y0 + rows) {          // parity diagnostics only
+        const int fx = ix > 0.f ? (ix < Wm1 ? 0 : 2) : 1, fy = iy > 0.f ? (iy < Hm1 ? 0 : 2) : 1;
+        sc.cell_map[(((long)sp * a.N + n) * H + R) * W + col] =
+            xi | (yi << PHOTO_CELL_YSHIFT) | (fx << PHOTO_CELL_FXSHIFT) | (fy << PHOTO_CELL_FYSHIFT);
+      }
       const uint32_t vo = (uint32_t)(yi * W + xi) * 4u;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
@@ -510,10 +518,7 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
 PhotoTiling photo_tiling(int W, int H, int N, int nscales) {
   PhotoTiling t;
   t.tiles_x = cdiv(W, PW);
-  static const int target = [] {
-    const char* e = std::getenv("MD2_PHOTO_WAVES");
-    return e ? std::max(1, std::atoi(e)) : PHOTO_WAVES;
-  }();
+  static const int target = std::max(1, tuning_knob("MD2_PHOTO_WAVES", PHOTO_WAVES));
   const double per_row = (double)nscales * N * t.tiles_x;
   int ty = (int)(target / per_row + 0.5);
   ty = std::max(1, std::min(ty, cdiv(H, 8)));
@@ -537,10 +542,24 @@ int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st)
   }
   const PhotoTiling tl = photo_tiling(g.W, g.H, a.N, a.nscales);
   const long blocks = tl.per_scale() * a.N * a.nscales;
-  if (C == 3)
-    hipLaunchKernelGGL(photo_stream_kernel<3>, dim3((unsigned)blocks), dim3(64), 0, st, a, g, tl);
+  bool cells = false;
+  for (int s = 0; s < a.nscales; ++s) cells |= a.sc[s].cell_map != nullptr;
+  if (cells) {
+    for (int s = 0; s < a.nscales; ++s)
+      if (!a.sc[s].cell_map) {
+        set_error("photometric: cell_map must be given for every scale or none");
+        return MD2_EINVAL;
+      }
+  }
+  const dim3 grid((unsigned)blocks), block(64);
+  if (C == 3 && !cells)
+    hipLaunchKernelGGL((photo_stream_kernel<3, false>), grid, block, 0, st, a, g, tl);
+  else if (C == 3)
+    hipLaunchKernelGGL((photo_stream_kernel<3, true>), grid, block, 0, st, a, g, tl);
+  else if (C == 1 && !cells)
+    hipLaunchKernelGGL((photo_stream_kernel<1, false>), grid, block, 0, st, a, g, tl);
   else if (C == 1)
-    hipLaunchKernelGGL(photo_stream_kernel<1>, dim3((unsigned)blocks), dim3(64), 0, st, a, g, tl);
+    hipLaunchKernelGGL((photo_stream_kernel<1, true>), grid, block, 0, st, a, g, tl);
   else {
     set_error("photometric: channels must be 1 or 3");
     return MD2_ENOTSUP;

@@ -35,6 +35,7 @@ class LossOut(C.Structure):
         ("loss", C.c_void_p), ("terms", C.c_void_p),
         ("d_disp", C.c_void_p * MAX_SCALES), ("d_pose", C.c_void_p),
         ("vis_loss", C.c_void_p), ("vis_sel", C.c_void_p), ("vis_warped", C.c_void_p),
+        ("vis_cell", C.c_void_p),
     ]
 
 
@@ -140,6 +141,7 @@ _SIGS = {
     "md2_grid_sample_border_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "md2_grid_sample_border_bwd": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                              P, P, P]),
+    "md2_unorm8_to_float": (C.c_int, [P, P, C.c_longlong, P]),
     "md2_smooth_loss_workspace_size": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
     "md2_smooth_loss_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
     "md2_smooth_loss_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, P, P, P]),

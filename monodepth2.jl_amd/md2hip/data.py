@@ -13,17 +13,29 @@ Mirrors the reference's datasets and loader:
   * ``DataLoader(dataset, batch_size)``  DataLoaders.jl as used by scripts/script.jl:90 --
     worker threads decode (PIL releases the GIL while decoding), batches are collated into
     pinned host memory in the library's layout ``x[N][3][C][H][W]`` (Julia ``(W,H,C,3,N)``,
-    same bytes) and copied to the GPU on a side stream, one batch ahead of the consumer.
-    With ``rank``/``world`` the sample order is sharded by global index (md2hip.dist).
+    same bytes) and copied to the GPU on a side stream, one batch ahead of the consumer.  The
+    N0f8 datasets (RGB Depth10k, KITTI) cross PCIe as BYTES and become Float32 on the GPU
+    (``md2_unorm8_to_float``: Float32(u) / 255f0, bit-identical to the host conversion) -- a
+    quarter of the H2D traffic and no float conversion on the host.  With ``rank``/``world``
+    the sample order is sharded by global index (md2hip.dist).
 
-Sample layout returned by ``__getitem__``: float32 numpy ``[3 frames][C][H][W]`` in [0, 1].
-Assumptions (third-party semantics, unpinned -- no reference test covers the loaders): Gray
-conversion uses the ITU-R BT.601 weights (0.299, 0.587, 0.114) of Colors.jl; ``imresize`` is
-restated as PIL bilinear resampling (ImageTransformations' interpolation / antialiasing filter is
-not reproduced bit-for-bit).
+Sample layout returned by ``__getitem__``: float32 numpy ``[3 frames][C][H][W]`` in [0, 1];
+``getobs_u8`` gives the same sample as the uint8 N0f8 bytes where the dataset's element type is
+N0f8 (RGB Depth10k, KITTI; not grayscale Depth10k, whose Gray{Float32} values are not bytes).
+Third-party semantics (unpinned -- no reference test or fixture covers the loaders):
+  * Gray conversion: the ITU-R BT.601 weights (0.299, 0.587, 0.114) of Colors.jl;
+  * ``imresize`` (ImageTransformations.jl, src/kitty.jl:52): restated from its published
+    algorithm (``imresize!``): the outer pixel corners of both images are mapped onto each other,
+    i.e. output pixel i (1-based) samples the input at ``sf * (i - 1/2) + 1/2`` with
+    ``sf = n_in / n_out`` per axis (clamped to [1, n_in] when upsampling), by
+    ``BSpline(Linear())`` interpolation (bilinear, NO antialiasing filter), and the result is
+    stored back in the input's element type -- N0f8 for the KITTI ``image_0`` PNGs, i.e. rounded
+    to the nearest 1/255.  Pinned here by known answers (tests/test_data.py) and cross-checked
+    against torch's ``interpolate(align_corners=False, antialias=False)``, the same map.
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 import queue
 import threading
@@ -37,17 +49,26 @@ from .dist import shard_range
 _GRAY = np.array([0.299, 0.587, 0.114], dtype=np.float32)
 
 
-def _load_png(path: str) -> np.ndarray:
-    """PNG -> float32 [C][H][W] in [0, 1] (N0f8 / N0f16 -> Float32, channelview)."""
+def _load_png_raw(path: str) -> np.ndarray:
+    """PNG -> its stored integers [C][H][W] (uint8 for N0f8, uint16 for N0f16 images)."""
     from PIL import Image
     with Image.open(path) as im:
         if im.mode in ("I;16", "I;16B", "I"):
-            a = np.asarray(im, dtype=np.float32) / 65535.0
-            return a[None]
+            return np.asarray(im, dtype=np.uint16)[None]
         if im.mode not in ("L", "RGB"):
             im = im.convert("RGB")
-        a = np.asarray(im, dtype=np.float32) / 255.0
+        a = np.asarray(im, dtype=np.uint8)
     return a[None] if a.ndim == 2 else np.ascontiguousarray(a.transpose(2, 0, 1))
+
+
+def _unorm(a: np.ndarray) -> np.ndarray:
+    """N0f8 / N0f16 -> Float32: Float32(u) / 255f0 (or 65535f0), as ``Float32.(channelview)``."""
+    return a.astype(np.float32) / np.float32(65535.0 if a.dtype == np.uint16 else 255.0)
+
+
+def _load_png(path: str) -> np.ndarray:
+    """PNG -> float32 [C][H][W] in [0, 1] (N0f8 / N0f16 -> Float32, channelview)."""
+    return _unorm(_load_png_raw(path))
 
 
 def _to_gray(chw: np.ndarray) -> np.ndarray:
@@ -56,13 +77,36 @@ def _to_gray(chw: np.ndarray) -> np.ndarray:
     return np.tensordot(_GRAY, chw, axes=(0, 0))[None].astype(np.float32)
 
 
-def _resize(chw: np.ndarray, height: int, width: int) -> np.ndarray:
+def _imresize_axis(n_in: int, n_out: int):
+    """Per output index: (i0, i1, f) of ``imresize!``'s sample position (module docstring)."""
+    sf = n_in / n_out
+    p = sf * (np.arange(1, n_out + 1, dtype=np.float64) - 0.5) + 0.5      # 1-based position
+    if sf < 1:
+        p = np.clip(p, 1.0, float(n_in))
+    p -= 1.0                                                              # 0-based
+    i0 = np.minimum(np.floor(p).astype(np.int64), n_in - 1)
+    f = p - i0
+    i1 = np.minimum(i0 + 1, n_in - 1)
+    return i0, i1, f
+
+
+def imresize(chw: np.ndarray, height: int, width: int) -> np.ndarray:
+    """``imresize(img, (height, width))`` of ImageTransformations.jl (src/kitty.jl:52) on
+    [C][H][W] images: bilinear at the outer-corner-aligned positions, no antialiasing; N0f8
+    (uint8) input -> N0f8 output rounded to the nearest 1/255 (the element type is kept), float
+    input -> float64 values."""
     if chw.shape[1:] == (height, width):
         return chw
-    from PIL import Image
-    out = np.empty((chw.shape[0], height, width), dtype=np.float32)
-    for c in range(chw.shape[0]):
-        out[c] = np.asarray(Image.fromarray(chw[c], mode="F").resize((width, height), Image.BILINEAR))
+    y0, y1, fy = _imresize_axis(chw.shape[1], height)
+    x0, x1, fx = _imresize_axis(chw.shape[2], width)
+    v = chw.astype(np.float64) / 255.0 if chw.dtype == np.uint8 else chw.astype(np.float64)
+    fx = fx[None, None, :]
+    fy = fy[None, :, None]
+    top = v[:, y0][:, :, x0] * (1 - fx) + v[:, y0][:, :, x1] * fx
+    bot = v[:, y1][:, :, x0] * (1 - fx) + v[:, y1][:, :, x1] * fx
+    out = top * (1 - fy) + bot * fy
+    if chw.dtype == np.uint8:
+        return np.rint(out * 255.0).astype(np.uint8)
     return out
 
 
@@ -87,11 +131,17 @@ class _Dataset:
     source_ids = (1, 3)
     target_id = 2
     augmentations = None
+    u8 = False                     # getobs_u8 gives the sample's N0f8 bytes
 
     def _augment(self, frames, i: int, seed: int):
         if self.augmentations is None:
             return frames
         return self.augmentations(frames, np.random.default_rng((seed, i)))
+
+    def getobs(self, i: int, seed: int = 0) -> np.ndarray:
+        return _unorm(self.getobs_u8(i, seed))
+
+    __getitem__ = getobs
 
 
 class Depth10k(_Dataset):
@@ -106,22 +156,34 @@ class Depth10k(_Dataset):
         self.dir, self.files = image_dir, list(image_files)
         self.augmentations, self.grayscale = augmentations, grayscale
         self.channels = 1 if grayscale else 3
+        self.u8 = not grayscale
 
     def __len__(self):
         return len(self.files)
 
-    def getobs(self, i: int, seed: int = 0) -> np.ndarray:
-        """Sample ``i`` (0-based): float32 [3][C][H][W] (dtk.jl:29-46)."""
+    def _frames(self, img, i, seed):
         width, height = self.resolution
-        img = _load_png(os.path.join(self.dir, self.files[i]))
-        if self.grayscale:
-            img = _to_gray(img)
         if img.shape[1] != height or img.shape[2] != 3 * width:
             raise ValueError(f"{self.files[i]}: expected {3 * width}x{height} triplet, got "
                              f"{img.shape[2]}x{img.shape[1]}")
         frames = [img[:, :, width * j:width * (j + 1)] for j in range(3)]
-        frames = self._augment(frames, i, seed)
-        return np.stack(frames, 0)
+        return np.stack(self._augment(frames, i, seed), 0)
+
+    def getobs_u8(self, i: int, seed: int = 0) -> np.ndarray:
+        """Sample ``i`` (0-based) as its N0f8 bytes: uint8 [3][3][H][W] (RGB only)."""
+        if self.grayscale:
+            raise TypeError("grayscale Depth10k samples are Gray{Float32}, not N0f8 bytes")
+        img = _load_png_raw(os.path.join(self.dir, self.files[i]))
+        if img.dtype != np.uint8:
+            raise TypeError(f"{self.files[i]}: not an 8-bit image")
+        return self._frames(img, i, seed)
+
+    def getobs(self, i: int, seed: int = 0) -> np.ndarray:
+        """Sample ``i`` (0-based): float32 [3][C][H][W] (dtk.jl:29-46)."""
+        img = _load_png(os.path.join(self.dir, self.files[i]))
+        if self.grayscale:
+            img = _to_gray(img)
+        return self._frames(img, i, seed)
 
     __getitem__ = getobs
 
@@ -153,22 +215,24 @@ class KittyDataset(_Dataset):
         self.total_length = n_frames // len(self.frame_ids)
         self.augmentations = augmentations
         self.channels = 1
+        self.u8 = True
 
     def __len__(self):
         return self.total_length
 
-    def getobs(self, i: int, seed: int = 0) -> np.ndarray:
-        """Sample ``i`` (0-based): frames 3i, 3i+1, 3i+2 (kitty.jl:47-61) -> [3][1][H][W]."""
+    def getobs_u8(self, i: int, seed: int = 0) -> np.ndarray:
+        """Sample ``i`` (0-based): frames 3i, 3i+1, 3i+2 (kitty.jl:47-61), each ``imresize``d to
+        the target size and kept N0f8 -> uint8 [3][1][H][W]."""
         width, height = self.resolution
         sid = i * len(self.frame_ids)
         frames = []
         for x in self.frame_ids:
-            img = _to_gray(_load_png(os.path.join(self.frames_dir, "%06d.png" % (sid + x - 1))))
-            frames.append(_resize(img, height, width))
+            img = _load_png_raw(os.path.join(self.frames_dir, "%06d.png" % (sid + x - 1)))
+            if img.dtype != np.uint8 or img.shape[0] != 1:
+                raise TypeError("KITTI image_0 frames are 8-bit grayscale")
+            frames.append(imresize(img, height, width))
         frames = self._augment(frames, i, seed)
         return np.stack(frames, 0)
-
-    __getitem__ = getobs
 
 
 class DChain:
@@ -179,6 +243,7 @@ class DChain:
         self.bins = np.cumsum([len(d) for d in self.datasets]).tolist()
         self.channels = self.datasets[0].channels
         self.resolution = self.datasets[0].resolution
+        self.u8 = all(getattr(d, "u8", False) for d in self.datasets)
 
     def __len__(self):
         return self.bins[-1] if self.bins else 0
@@ -188,6 +253,12 @@ class DChain:
             raise IndexError(i)
         bid = next(b for b, edge in enumerate(self.bins) if i < edge)
         return self.datasets[bid].getobs(i - (self.bins[bid - 1] if bid else 0), seed)
+
+    def getobs_u8(self, i: int, seed: int = 0) -> np.ndarray:
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        bid = next(b for b, edge in enumerate(self.bins) if i < edge)
+        return self.datasets[bid].getobs_u8(i - (self.bins[bid - 1] if bid else 0), seed)
 
     __getitem__ = getobs
 
@@ -199,12 +270,15 @@ class DataLoader:
     world`` is cut into per-rank shards by global index (md2hip.dist.shard_range), so the union
     over ranks is identical for every GPU count.  Incomplete trailing batches are dropped
     (fixed-shape train step).  ``workers`` decode threads; one batch is prefetched and its
-    host->device copy runs on a side stream while the previous batch trains."""
+    host->device copy runs on a side stream while the previous batch trains.  ``bytes_h2d``
+    (default): N0f8 datasets are copied as uint8 and converted on the GPU."""
 
     def __init__(self, dataset, batch_size: int, *, shuffle: bool = True, seed: int = 0,
-                 workers: int = 8, device=None, rank: int = 0, world: int = 1, prefetch: int = 2):
+                 workers: int = 8, device=None, rank: int = 0, world: int = 1, prefetch: int = 2,
+                 bytes_h2d: bool = True):
         self.ds, self.batch_size, self.shuffle, self.seed = dataset, batch_size, shuffle, seed
         self.workers, self.rank, self.world, self.prefetch = workers, rank, world, prefetch
+        self.bytes_h2d = bytes_h2d
         self.device = device
         self.epoch = 0
 
@@ -234,18 +308,30 @@ class DataLoader:
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
         stop = threading.Event()
 
+        use_u8 = on_gpu and self.bytes_h2d and getattr(self.ds, "u8", False)
+        if use_u8:
+            from ._lib import check, lib, ptr
+            get = lambda i: self.ds.getobs_u8(i, seed=self.seed + epoch)
+        else:
+            get = lambda i: self.ds.getobs(i, seed=self.seed + epoch)
+
         def produce():
             try:
                 with ThreadPoolExecutor(self.workers) as pool:
                     for idx in batches:
                         if stop.is_set():
                             return
-                        samples = list(pool.map(lambda i: self.ds.getobs(i, seed=self.seed + epoch), idx))
-                        host = torch.from_numpy(np.stack(samples, 0))
+                        host = torch.from_numpy(np.stack(list(pool.map(get, idx)), 0))
                         if on_gpu:
                             host = host.pin_memory()
                             with torch.cuda.stream(stream):
                                 x = host.to(dev, non_blocking=True)
+                                if use_u8:          # N0f8 bytes -> Float32 on the GPU
+                                    xf = torch.empty(x.shape, dtype=torch.float32, device=dev)
+                                    check(lib().md2_unorm8_to_float(ptr(x), ptr(xf), x.numel(),
+                                                                    C.c_void_p(stream.cuda_stream)),
+                                          "md2_unorm8_to_float")
+                                    x = xf
                                 ev = torch.cuda.Event()
                                 ev.record(stream)
                             q.put((x, ev, host))

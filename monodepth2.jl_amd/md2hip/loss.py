@@ -113,6 +113,8 @@ def loss_tail(disparities, poses, x, auto_loss, cache: TrainCache, params: Param
         res["vis_loss"] = torch.empty(len(disparities), N, H, W, dtype=torch.float32, device=dev)
         res["vis_sel"] = torch.empty(len(disparities), N, H, W, dtype=torch.int8, device=dev)
         res["vis_warped"] = torch.empty(2, N, C_, H, W, dtype=torch.float32, device=dev)
+        # per-pixel bilinear cells / border states of both sources (parity diagnostics)
+        res["vis_cell"] = torch.empty(len(disparities), 2, N, H, W, dtype=torch.int32, device=dev)
     am = None
     if params.automasking:
         if auto_loss is None:        # automasking_loss(ssim, x, target; source_ids), on the GPU
@@ -128,6 +130,7 @@ def loss_tail(disparities, poses, x, auto_loss, cache: TrainCache, params: Param
     out.vis_loss = res["vis_loss"].data_ptr() if visualize else None
     out.vis_sel = res["vis_sel"].data_ptr() if visualize else None
     out.vis_warped = res["vis_warped"].data_ptr() if visualize else None
+    out.vis_cell = res["vis_cell"].data_ptr() if visualize else None
     disp_arr = ptr_array(disparities)
     check(lib().md2_loss_fwd_bwd(C.byref(cfg), C.cast(disp_arr, _lib.FP), ptr(pose), ptr(x), ptr(am),
                                  C.c_float(dloss), C.byref(out), ptr(ws), stream_of(dev)),

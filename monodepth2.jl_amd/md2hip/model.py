@@ -153,7 +153,8 @@ class _Executor:
         self.handle = h
         self.nseg = lib().md2_model_num_segments(h)
         self.automask = params.automasking
-        self.forwarded = False
+        self.forwarded = False              # a forward_loss ran since the last eval_disparity here
+        self.pending = False                # ... and its backward has not run yet
         self.version = -1                   # Model.version its packed conv weights reflect
         self.sync()
 
@@ -208,7 +209,7 @@ class _Executor:
         am = auto_loss.contiguous() if (self.automask and auto_loss is not None) else None
         check(lib().md2_model_forward_loss(self.handle, ptr(x), ptr(am), ptr(loss), ptr(terms),
                                            stream_of(x.device)), "md2_model_forward_loss")
-        self.forwarded = True
+        self.forwarded = self.pending = True
         return loss
 
     def train_step_graph(self, x, opt: "ADAM", auto_loss=None, loss=None):
@@ -241,7 +242,9 @@ class _Executor:
         return off.value, ln.value
 
     def backward(self):
-        return [self.backward_segment(k) for k in range(self.nseg)]
+        r = [self.backward_segment(k) for k in range(self.nseg)]
+        self.pending = False
+        return r
 
     def outputs(self):
         """(disparities [N,1,h,w] views, poses [2N,6] view) of the last forward (device memory
@@ -341,8 +344,11 @@ class Model:
 
     def eval_executor(self, N, H, W) -> _Executor:
         """An executor of batch >= N at (H, W) for eval_disparity (the loss configuration does not
-        matter for inference); a new one (default TrainCache/Params) only if none fits."""
-        fits = [ex for k, ex in self._ex.items() if k[1] == H and k[2] == W and k[0] >= N]
+        matter for inference) that holds no pending train forward -- inference overwrites the
+        executor's activations, so an executor between train_loss and gradient() is never taken;
+        a new one (default TrainCache/Params) only if none fits."""
+        fits = [ex for k, ex in self._ex.items() if k[1] == H and k[2] == W and k[0] >= N
+                and not ex.pending]
         if fits:
             ex = min(fits, key=lambda e: e.batch)
             ex.sync()
@@ -352,6 +358,7 @@ class Model:
         params = Params(target_size=(W, H), batch_size=N, automasking=False)
         key = (N, H, W, tuple(np.asarray(cache.K).reshape(-1)), tuple(cache.scales), params.min_depth,
                params.max_depth, params.disparity_smoothness, params.automasking)
+        key = key + ("eval",) if key in self._ex else key          # that one has a pending forward
         ex = self._ex[key] = _Executor(self, N, H, W, cache, params)   # leaves _last (training) alone
         return ex
 
@@ -473,6 +480,7 @@ def eval_disparity(model: Model, x, cache: Optional[TrainCache] = None):
         raise ValueError("x must be [N, in_channels, H, W]")
     ex = model.eval_executor(N, H, W)
     dptr = (C.c_void_p * 5)()
+    ex.forwarded = False            # the library discards any pending forward of this executor
     check(lib().md2_model_eval_disparity(ex.handle, ptr(x), N, dptr, stream_of(x.device)),
           "md2_model_eval_disparity")
     out = []

@@ -183,6 +183,42 @@ def grid_sample_border(image: torch.Tensor, grid: torch.Tensor) -> torch.Tensor:
     return F.grid_sample(image, grid, mode="bilinear", padding_mode="border", align_corners=True)
 
 
+def grid_sample_border_forced(image: torch.Tensor, grid: torch.Tensor, cell: torch.Tensor):
+    """Test hook (like ``_forced_min``): ``grid_sample_border`` with the bilinear cell and the
+    border-clamp state of every sample IMPOSED.  ``cell`` [N,H,W] int32 packs the 0-based cell
+    corner x | y << 12 and the border states sx << 24 | sy << 26 (0 = interior: the coordinate
+    itself, differentiable; 1 = clamped to 0; 2 = clamped to W-1 / H-1: constant) -- the GPU's
+    own decisions (md2_loss_out.vis_cell).  Where the decisions agree with the unforced sampler
+    the value and gradient are NNlib's (align_corners unnormalise ((g+1)/2)(W-1), border clamp
+    with a zero gradient where clamped, bilinear interpolation in the floor cell); where fp32 and
+    fp64 sit on opposite sides of a cell edge or of the border, the forced sampler uses the
+    linear continuation of the GPU's cell, so both evaluate the same smooth function."""
+    N, C, H, W = image.shape
+    Ho, Wo = grid.shape[1], grid.shape[2]
+    dt = image.dtype
+    ix = (grid[..., 0] + 1.0) * 0.5 * (W - 1)
+    iy = (grid[..., 1] + 1.0) * 0.5 * (H - 1)
+    cell = cell.long()
+    xi, yi = cell & 0xFFF, (cell >> 12) & 0xFFF
+    sx, sy = (cell >> 24) & 3, (cell >> 26) & 3
+    xc = torch.where(sx == 0, ix, torch.where(sx == 1, torch.zeros((), dtype=dt),
+                                              torch.full((), W - 1.0, dtype=dt)))
+    yc = torch.where(sy == 0, iy, torch.where(sy == 1, torch.zeros((), dtype=dt),
+                                              torch.full((), H - 1.0, dtype=dt)))
+    fx = (xc - xi.to(dt)).unsqueeze(1)
+    fy = (yc - yi.to(dt)).unsqueeze(1)
+    flat = image.reshape(N, C, H * W)
+
+    def tap(yy, xx):
+        idx = (yy * W + xx).reshape(N, 1, Ho * Wo).expand(N, C, Ho * Wo)
+        return flat.gather(2, idx).reshape(N, C, Ho, Wo)
+
+    v00, v01, v10, v11 = tap(yi, xi), tap(yi, xi + 1), tap(yi + 1, xi), tap(yi + 1, xi + 1)
+    top = v00 + fx * (v01 - v00)
+    bot = v10 + fx * (v11 - v10)
+    return top + fy * (bot - top)
+
+
 def grid_sample_zeros(image: torch.Tensor, grid: torch.Tensor) -> torch.Tensor:
     """NNlib ``grid_sample(x, grid)`` default ``padding_mode=:zeros`` (test/runtests.jl:116)."""
     return F.grid_sample(image, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
@@ -249,18 +285,22 @@ def apply_mask(mask: torch.Tensor, warp_loss: torch.Tensor):
     return _first_argmin([mask, warp_loss])
 
 
-def warp(disparity_full, x, Ps, K, invK, source_ids, min_depth, max_depth):
+def warp(disparity_full, x, Ps, K, invK, source_ids, min_depth, max_depth, cells=None):
     """The per-scale warp body of ``train_loss`` (src/training.jl:48-57).  Also the definition of
     the ``warp`` that ``slow_depth`` calls but the reference never defines (defect D1).
-    disparity_full [N,1,H,W]; x [N,L,C,H,W]; Ps = [(R [N,3,3], t [N,3])] per source."""
+    disparity_full [N,1,H,W]; x [N,L,C,H,W]; Ps = [(R [N,3,3], t [N,3])] per source.
+    ``cells``: test hook, per source the imposed bilinear cells (grid_sample_border_forced)."""
     N, _, H, W = disparity_full.shape
     depth = disparity_to_depth(disparity_full, min_depth, max_depth)
     coords = backproject(depth.reshape(N, 1, H * W), invK, W, H)
     warped = []
-    for (R, t), sid in zip(Ps, source_ids):
+    for j, ((R, t), sid) in enumerate(zip(Ps, source_ids)):
         uv = project(coords, K, R, t, W, H)                       # [N,2,P]
         grid = uv.reshape(N, 2, H, W).permute(0, 2, 3, 1)         # [N,H,W,2]
-        warped.append(grid_sample_border(x[:, sid - 1], grid))
+        if cells is not None:
+            warped.append(grid_sample_border_forced(x[:, sid - 1], grid, cells[j]))
+        else:
+            warped.append(grid_sample_border(x[:, sid - 1], grid))
     return warped
 
 
@@ -280,9 +320,12 @@ def _forced_min(cands: Sequence[torch.Tensor], sel: torch.Tensor) -> torch.Tenso
 
 
 def loss_from_outputs(disparities, poses, x, auto_loss, cache: TrainCache, params: Params,
-                      return_parts: bool = False, forced_sel=None, per_source=None):
+                      return_parts: bool = False, forced_sel=None, per_source=None,
+                      forced_cells=None):
     """The body of ``train_loss`` after the model call -- src/training.jl:25,29-77.
-    disparities: list of [N,1,h,w] (one per scale); poses: list of (rvec [N,3], tvec [N,3])."""
+    disparities: list of [N,1,h,w] (one per scale); poses: list of (rvec [N,3], tvec [N,3]).
+    Test hooks: ``forced_sel`` (per scale, the imposed argmin), ``forced_cells`` (per scale
+    [2,N,H,W], the imposed bilinear cells / border states of both sources)."""
     width, height = params.target_size
     target_x = x[:, cache.target_id - 1]
     Ps = poses_to_transforms(poses, cache.source_ids, cache.target_id)
@@ -292,7 +335,8 @@ def loss_from_outputs(disparities, poses, x, auto_loss, cache: TrainCache, param
         if disparity.shape[-1] != width or disparity.shape[-2] != height:
             disparity = upsample_bilinear_size(disparity, (height, width))
         warped = warp(disparity, x, Ps, cache.K, cache.invK, cache.source_ids,
-                      params.min_depth, params.max_depth)
+                      params.min_depth, params.max_depth,
+                      cells=None if forced_cells is None else forced_cells[len(parts)])
         src_losses = [photometric_loss(p, target_x) for p in warped]
         if per_source is not None:
             per_source.append([l.detach() for l in src_losses])

@@ -1,5 +1,19 @@
 """Full train-step parity helper: GPU Model (libmd2hip) vs the fp64 CPU oracle on the same
-flat parameters and inputs, with the GPU's per-pixel argmin imposed on the oracle."""
+flat parameters and inputs, with the GPU's branch decisions imposed on the oracle.
+
+The objective is piecewise smooth.  Its branch decisions are: the per-pixel argmin over sources
+(src/training.jl:13-15), ReLU masks and max-pool argmax (encoder / pose decoder), and grid_sample's
+bilinear cell and border clamp (src/training.jl:56).  A decision whose inputs sit within fp32
+rounding of its switching point flips between the fp32 GPU and the fp64 oracle, and one flipped
+decision moves the gradient by O(1) at that pixel.  Each decision the GPU made is therefore
+recorded (``vis_sel``, ``vis_cell``, ``md2_model_debug_tensor``) and imposed on the oracle
+(``forced_sel``, ``forced_cells``, ``O.forced_decisions``); the oracle then evaluates the same
+smooth function as the GPU, and the comparison is pure fp32-vs-fp64 accuracy.
+
+Source frames (``sources``):
+  "ramp"     affine ramps (bilinear sampling of them has no kinks at all),
+  "texture"  low-frequency texture + 15 % pixel noise (tests/_data.py),
+  "uniform"  the bench's own i.i.d. U[0,1) triplets (md2hip.dist.synthetic_triplets)."""
 import torch
 
 import md2hip
@@ -10,9 +24,21 @@ from tests import _data as D
 DEFAULT_SCALES = {1: 0.0625, 2: 0.125, 3: 0.25, 4: 0.5, 5: 1.0}
 
 
+def inputs(N, C, H, W, sources="ramp", seed=7):
+    if sources == "uniform":
+        from md2hip.dist import synthetic_triplets
+        return synthetic_triplets(N, H, W, 0, "cpu", channels=C).double()
+    return D.triplets(N, C, H, W, seed=seed, ramp_sources=(sources == "ramp"))
+
+
+def _sources(strict, sources):
+    return sources if sources is not None else ("ramp" if strict else "texture")
+
+
 def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, automasking=False, levels=(2, 3, 4, 5),
-        target_id=2, source_ids=(1, 3)):
-    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
+        target_id=2, source_ids=(1, 3), sources=None):
+    sources = _sources(strict, sources)
+    x = inputs(N, C, H, W, sources, seed)
     K, invK = D.intrinsics(W, H)
     enc = md2hip.ResNet(arch, in_channels=C)
     model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=list(levels),
@@ -32,7 +58,8 @@ def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, automasking=False, 
     torch.cuda.synchronize()
     g = {"loss": loss.item(), "tail_loss": tail["loss"].item(), "disps": [d.cpu() for d in disps],
          "pose": pose.cpu(), "grad": model.grad.cpu(), "sel": tail["vis_sel"].cpu(),
-         "flat": model.flat.detach().double().cpu()}
+         "cells": tail["vis_cell"].cpu(), "flat": model.flat.detach().double().cpu(),
+         "x": x, "sources": sources, "automasking": automasking}
     g["decisions"] = gpu_decisions(model, N, arch, target_id=target_id, source_ids=source_ids)
     spec = O.param_spec(arch, C, tuple(levels))
     flat = model.flat.detach().double().cpu().clone().requires_grad_(True)
@@ -44,21 +71,23 @@ def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, automasking=False, 
     # the GPU's argmin (-1 = automask) as an index into [auto_loss?, source 0, source 1]
     forced = [g["sel"][s].unsqueeze(1).long() + (1 if automasking else 0) for s in range(len(levels))]
     auto_o = O.automasking_loss(x, x[:, target_id - 1], source_ids) if automasking else None
-    loss_o = O.loss_from_outputs(d_o, p_o, x, auto_o, cache_o, par_o, forced_sel=forced)
+    loss_o = O.loss_from_outputs(d_o, p_o, x, auto_o, cache_o, par_o, forced_sel=forced,
+                                 forced_cells=g["cells"])
     loss_o.backward()
     o = {"loss": loss_o.item(), "disps": [d.detach() for d in d_o],
          "pose": torch.cat([torch.cat([r, t], 1) for r, t in p_o], 0).detach(), "grad": flat.grad}
-    errs = {}
-    for name, shape, off in [(n, s, None) for n, s in spec]:
-        pass
-    off = 0
+    return g, o, per_tensor(spec, g["grad"], o["grad"])
+
+
+def per_tensor(spec, a, b):
+    errs, off = {}, 0
     for name, shape in spec:
         n = 1
         for s in shape:
             n *= s
-        errs[name] = D.rel_err(g["grad"][off:off + n], o["grad"][off:off + n])
+        errs[name] = D.rel_err(a[off:off + n], b[off:off + n])
         off += n
-    return g, o, errs
+    return errs
 
 
 def gpu_decisions(model, N, arch=18, L=3, target_id=2, source_ids=(1, 3)):
@@ -88,67 +117,87 @@ def gpu_decisions(model, N, arch=18, L=3, target_id=2, source_ids=(1, 3)):
     return d
 
 
-def oracle_at_gpu_outputs(g, N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7):
-    """The fp64 oracle's gradient with the loss tail evaluated AT THE GPU's forward outputs
-    (disparities, poses) and back-propagated through the oracle's own networks (value substituted,
-    graph kept: d_o + (d_gpu - d_o).detach()).  Against the plain oracle this isolates how much
-    of a gradient difference the ~1e-6 forward discrepancy alone explains; against the GPU it
-    measures the backward's own accuracy."""
-    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
-    K, invK = D.intrinsics(W, H)
-    spec = O.param_spec(arch, C, (2, 3, 4, 5))
-    f = g["flat"].double().clone().requires_grad_(True)
-    P = O.unflatten(f, spec)
-    with O.forced_decisions(g["decisions"]):
-        d_o, p_o = O.model_forward(P, x, arch=arch)
-    d_s = [d + (dg.double().view_as(d) - d).detach() for d, dg in zip(d_o, g["disps"])]
-    pg = g["pose"].double()
-    p_s = []
-    for k, (r, t) in enumerate(p_o):
-        q = pg[k * N:(k + 1) * N]
-        p_s.append((r + (q[:, :3] - r).detach(), t + (q[:, 3:] - t).detach()))
-    cache_o = O.TrainCache(K=K, invK=invK)
-    par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
-    forced = [s.unsqueeze(1).long() for s in g["sel"]]
-    O.loss_from_outputs(d_s, p_s, x, None, cache_o, par_o, forced_sel=forced).backward()
-    return f.grad.double()
-
-
-def oracle_fp32_floor(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, flat=None, sel=None,
-                      decisions=None, levels=(2, 3, 4, 5), target_id=2, source_ids=(1, 3)):
-    """Per-tensor gradient error of the SAME oracle run in fp32 vs fp64 (the fp32 noise floor),
-    plus the forward outputs' floors under the keys "__disp<s>" and "__pose"."""
-    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=strict)
+def _oracle_grad(g, dt, arch, levels, target_id, source_ids, perturb=None, seed=0):
+    """The oracle's flat gradient in dtype ``dt`` with every GPU decision imposed.  ``perturb``:
+    relative std of i.i.d. noise added to the loss tail's inputs (the disparities and poses the
+    networks hand to train_loss), value substituted with the graph kept."""
+    x = g["x"]
+    N, L, C, H, W = x.shape
     K, invK = D.intrinsics(W, H)
     spec = O.param_spec(arch, C, tuple(levels))
     scales = tuple(DEFAULT_SCALES[l] for l in levels)
-    grads, fwd, losses = [], [], []
-    for dt in (torch.float64, torch.float32):
-        f = flat.to(dt).clone().requires_grad_(True)
-        P = O.unflatten(f, spec)
-        with O.forced_decisions(decisions or {}):
-            d_o, p_o = O.model_forward(P, x.to(dt), source_ids, target_id, arch=arch,
-                                       scale_levels=tuple(levels))
-        fwd.append(([d.detach().double() for d in d_o],
-                    torch.cat([torch.cat([r, t], 1) for r, t in p_o], 0).detach().double()))
-        cache_o = O.TrainCache(K=K.to(dt), invK=invK.to(dt), target_id=target_id,
-                               source_ids=tuple(source_ids), scales=scales)
-        par_o = O.Params(target_size=(W, H), batch_size=N, automasking=False)
-        forced = [s.unsqueeze(1).long() for s in sel]
-        lo = O.loss_from_outputs(d_o, p_o, x.to(dt), None, cache_o, par_o, forced_sel=forced)
-        lo.backward()
-        losses.append(lo.item())
-        grads.append(f.grad.double())
-    errs, off = {}, 0
-    for name, shape in spec:
-        n = 1
-        for s in shape:
-            n *= s
-        errs[name] = D.rel_err(grads[1][off:off + n], grads[0][off:off + n])
-        off += n
-    # forward outputs: "__disp<s>" per scale and "__pose"
-    for s_, (a, b) in enumerate(zip(fwd[1][0], fwd[0][0])):
-        errs[f"__disp{s_}"] = D.rel_err(a, b)
-    errs["__pose"] = D.rel_err(fwd[1][1], fwd[0][1])
-    errs["__loss"] = abs(losses[1] - losses[0]) / abs(losses[0])
-    return errs
+    f = g["flat"].to(dt).clone().requires_grad_(True)
+    P = O.unflatten(f, spec)
+    with O.forced_decisions(g["decisions"]):
+        d_o, p_o = O.model_forward(P, x.to(dt), source_ids, target_id, arch=arch,
+                                   scale_levels=tuple(levels))
+    if perturb:
+        gen = torch.Generator().manual_seed(seed)
+        noise = lambda t: t + (t * perturb * torch.randn(t.shape, generator=gen, dtype=t.dtype)).detach()
+        d_o = [noise(d) for d in d_o]
+        p_o = [(noise(r), noise(t)) for r, t in p_o]
+    cache_o = O.TrainCache(K=K.to(dt), invK=invK.to(dt), target_id=target_id,
+                           source_ids=tuple(source_ids), scales=scales)
+    am = g["automasking"]
+    par_o = O.Params(target_size=(W, H), batch_size=N, automasking=am)
+    forced = [s.unsqueeze(1).long() + (1 if am else 0) for s in g["sel"]]
+    auto_o = O.automasking_loss(x.to(dt), x[:, target_id - 1].to(dt), source_ids) if am else None
+    lo = O.loss_from_outputs(d_o, p_o, x.to(dt), auto_o, cache_o, par_o, forced_sel=forced,
+                             forced_cells=g["cells"])
+    lo.backward()
+    fwd = ([d.detach().double() for d in d_o], torch.cat([torch.cat([r, t], 1) for r, t in p_o], 0).detach().double())
+    return f.grad.double(), fwd, lo.item(), spec
+
+
+def oracle_bounds(g, o=None, eps=2.0 ** -23, arch=18, levels=(2, 3, 4, 5), target_id=2,
+                  source_ids=(1, 3)):
+    """Two references for judging the GPU gradient, both from the oracle with every GPU decision
+    imposed:
+      floor[k]  per-tensor error of the SAME oracle run in fp32 vs fp64 (the fp32 noise floor),
+                plus the forward outputs' floors under "__disp<s>", "__pose", "__loss";
+      sens[k]   per-tensor relative change of the fp64 gradient when the loss tail's inputs (the
+                disparities and poses the networks hand to train_loss) carry relative noise of
+                one fp32 ulp (``eps``): how far an fp32-accurate forward can legitimately move
+                that gradient.  Large for cancelling sums -- e.g. a decoder head's bias gradient,
+                a sum of ~1e6 full-resolution pixel gradients of both signs.
+    ``o``: the fp64 result of ``run`` (its gradient is the unperturbed base); recomputed if None."""
+    kw = dict(arch=arch, levels=levels, target_id=target_id, source_ids=source_ids)
+    if o is None:
+        g64, f64, l64, spec = _oracle_grad(g, torch.float64, **kw)
+    else:
+        g64, f64, l64 = o["grad"].double(), (o["disps"], o["pose"]), o["loss"]
+        spec = O.param_spec(arch, g["x"].shape[2], tuple(levels))
+    g32, f32, l32, _ = _oracle_grad(g, torch.float32, **kw)
+    floor = per_tensor(spec, g32, g64)
+    for s_, (a, b) in enumerate(zip(f32[0], f64[0])):
+        floor[f"__disp{s_}"] = D.rel_err(a, b)
+    floor["__pose"] = D.rel_err(f32[1], f64[1])
+    floor["__loss"] = abs(l32 - l64) / abs(l64)
+    pert, _, _, _ = _oracle_grad(g, torch.float64, perturb=eps, seed=1, **kw)
+    sens = per_tensor(spec, pert, g64)
+    return floor, sens
+
+
+def grad_bounds(floor, sens, abs_floor=2e-5):
+    """Per-tensor gradient bound: 4x the oracle's own fp32 floor, 4x its 1-ulp forward
+    sensitivity, and an absolute floor for the accumulation-order noise of well-conditioned
+    tensors (the GPU sums in other orders than torch-CPU)."""
+    return {k: max(4 * floor[k], 4 * sens[k], abs_floor) for k in sens}
+
+
+def check_step(g, o, errs, floor, sens, label=""):
+    """The full-step assertions shared by the model parity tests: loss, forward outputs, and every
+    gradient tensor within its bound (grad_bounds).  Prints the tightest margins."""
+    assert abs(g["loss"] - o["loss"]) <= max(1e-6, 4 * floor["__loss"]) * abs(o["loss"]), \
+        (g["loss"], o["loss"], floor["__loss"])
+    for s_, (a, b) in enumerate(zip(g["disps"], o["disps"])):
+        assert D.rel_err(a, b) < max(1e-5, 4 * floor[f"__disp{s_}"]), s_
+    assert D.rel_err(g["pose"], o["pose"]) < max(1e-5, 4 * floor["__pose"])
+    bound = grad_bounds(floor, sens)
+    ratio = sorted(((errs[k] / bound[k], k) for k in bound), reverse=True)
+    print(f"\n{label} loss {g['loss']:.7f} vs {o['loss']:.7f}; tightest err/bound: " +
+          ", ".join(f"{k} {errs[k]:.2e}/{bound[k]:.2e} (floor {floor[k]:.1e}, sens {sens[k]:.1e})"
+                    for _, k in ratio[:4]))
+    bad = {k: (errs[k], bound[k]) for k in bound if errs[k] > bound[k]}
+    assert not bad, bad
+    return max(errs.values())

@@ -130,3 +130,67 @@ def test_dataloader_surfaces_decode_errors(tmp_path):
     ds = md2hip.Depth10k(str(tmp_path), ["bad.png"])
     with pytest.raises(Exception):
         list(md2hip.DataLoader(ds, 1, shuffle=False, workers=1))
+
+
+def test_imresize_known_answers():
+    """ImageTransformations.imresize restated (md2hip.data.imresize; src/kitty.jl:52): output
+    pixel i samples the input at sf*(i - 1/2) + 1/2 (1-based) bilinearly, no antialiasing."""
+    from md2hip.data import imresize
+    rng = np.random.default_rng(3)
+    # constant -> constant, both directions
+    c = np.full((1, 10, 14), 77, dtype=np.uint8)
+    assert (imresize(c, 4, 5) == 77).all() and (imresize(c, 23, 31) == 77).all()
+    # an exact 2x downsample is the 2x2 box average (sample points fall between pixel pairs)
+    a = rng.integers(0, 256, (1, 8, 12)).astype(np.float64)
+    box = a.reshape(1, 4, 2, 6, 2).mean(axis=(2, 4))
+    np.testing.assert_allclose(imresize(a, 4, 6), box, rtol=0, atol=1e-12)
+    # N0f8 in -> N0f8 out: rounded to the nearest 1/255 (round half to even)
+    u = np.array([[[0, 1, 2, 3]]], dtype=np.uint8)
+    np.testing.assert_array_equal(imresize(u, 1, 2), [[[0, 2]]])        # 0.5 -> 0, 2.5 -> 2
+    # an affine ramp is reproduced exactly at the mapped coordinates (bilinear of affine)
+    H0, W0, H1, W1 = 37, 53, 16, 24
+    yy, xx = np.meshgrid(np.arange(H0), np.arange(W0), indexing="ij")
+    ramp = (0.3 * xx + 0.7 * yy + 2.0)[None].astype(np.float64)
+    py = (H0 / H1) * (np.arange(1, H1 + 1) - 0.5) + 0.5 - 1
+    px = (W0 / W1) * (np.arange(1, W1 + 1) - 0.5) + 0.5 - 1
+    np.testing.assert_allclose(imresize(ramp, H1, W1)[0], 0.3 * px[None, :] + 0.7 * py[:, None] + 2.0,
+                               rtol=0, atol=1e-12)
+    # upsampling clamps the sample positions to the image
+    up = imresize(np.array([[[0.0, 1.0]]]), 1, 4)
+    np.testing.assert_allclose(up, [[[0.0, 0.25, 0.75, 1.0]]], atol=1e-12)
+
+
+def test_imresize_matches_half_pixel_bilinear():
+    """The same map as torch's interpolate(align_corners=False, antialias=False), at KITTI's
+    1241x376 -> 416x128 and for an upsample (cross-check of the restatement, in fp64)."""
+    import torch.nn.functional as F
+    from md2hip.data import imresize
+    rng = np.random.default_rng(4)
+    for (h0, w0, h1, w1) in [(376, 1241, 128, 416), (20, 30, 64, 90)]:
+        a = rng.random((1, h0, w0))
+        ref = F.interpolate(torch.from_numpy(a)[None], size=(h1, w1), mode="bilinear",
+                            align_corners=False, antialias=False)[0].numpy()
+        np.testing.assert_allclose(imresize(a, h1, w1), ref, rtol=0, atol=1e-12)
+
+
+def test_u8_samples_match_float_samples(dtk, tmp_path):
+    """getobs_u8 is the same sample as getobs, as bytes: Float32(u) / 255f0 of it is bit-identical
+    (RGB Depth10k with FlipX, KITTI after imresize); grayscale Depth10k has no byte form."""
+    import md2hip
+    from md2hip.data import _unorm
+    d, files = dtk
+    ds = md2hip.Depth10k(d, files, augmentations=md2hip.FlipX(0.5))
+    for i in range(len(ds)):
+        np.testing.assert_array_equal(_unorm(ds.getobs_u8(i, seed=2)), ds.getobs(i, seed=2))
+    with pytest.raises(TypeError):
+        md2hip.Depth10k(d, files, grayscale=True).getobs_u8(0)
+    seq = tmp_path / "k" / "sequences" / "00" / "image_0"
+    seq.mkdir(parents=True)
+    (tmp_path / "k" / "sequences" / "00" / "calib.txt").write_text("P0: " + " ".join(["1.0"] * 12) + "\n")
+    rng = np.random.default_rng(5)
+    for k in range(3):
+        Image.fromarray(rng.integers(0, 256, (376, 1241)).astype(np.uint8), mode="L").save(str(seq / ("%06d.png" % k)))
+    kd = md2hip.KittyDataset(str(tmp_path / "k"), "00", target_size=(128, 416))
+    u = kd.getobs_u8(0)
+    assert u.dtype == np.uint8 and u.shape == (3, 1, 128, 416)
+    np.testing.assert_array_equal(_unorm(u), kd[0])

@@ -53,3 +53,52 @@ def test_fused_splitk_bn_bitwise(B, H, W, switch):
         assert torch.equal(lf, lu), (i, lf, lu)
         assert torch.equal(mf.flat, mu.flat), i
         assert torch.equal(of.m, ou.m) and torch.equal(of.v, ou.v), i
+
+
+_KNOB_CHILD = r"""
+import os, sys
+root, out = sys.argv[1], sys.argv[2]
+sys.path[:0] = [root, os.path.join(root, "monodepth2.jl_amd")]
+import numpy as np, torch, md2hip, md2hip.dist
+from tests import _data as D
+B, H, W = 2, 64, 128
+enc = md2hip.ResNet(18, in_channels=3)
+m = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
+                                          embedding_levels=0), md2hip.PoseDecoder(512), seed=42)
+K, invK = D.intrinsics(W, H)
+ex = m.executor((B, 3, 3, H, W), md2hip.TrainCache(K=K.numpy(), invK=invK.numpy()),
+                md2hip.Params(target_size=(W, H), batch_size=B, automasking=False))
+opt = md2hip.ADAM(1e-4)
+for s in (5, 6):
+    md2hip.dist.train_step(ex, m, opt, D.triplets(B, 3, H, W, seed=s).float().cuda().contiguous(),
+                           md2hip.dist.GradAllReduce(force=False))
+torch.cuda.synchronize()
+np.save(out, m.flat.cpu().numpy())
+"""
+
+# settings every one of which an A/B sweep has run before (tools/*_sweep.sh, tools/ab_*.sh)
+KNOBS = {"MD2_PX_TARGET": "1024", "MD2_W_TILE": "2", "MD2_W_TARGET": "1024", "MD2_PX_V2": "0",
+         "MD2_HEAD_STRIP": "0", "MD2_UP_TILED": "0", "MD2_PHOTO_WAVES": "1024", "MD2_W16": "0",
+         "MD2_PX16": "0"}
+
+
+@pytest.mark.timeout(240)
+def test_tuning_knobs_ignored_without_md2_tuning(tmp_path):
+    """The kernel / planner tuning knobs (common.h tuning_knob) change nothing unless MD2_TUNING=1:
+    two steps with nine knobs set (and no MD2_TUNING) give bit-identical parameters to a clean
+    environment; with MD2_TUNING=1 the same knobs do take effect (other kernels, other roundings)."""
+    import subprocess
+    import sys
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = {k: v for k, v in os.environ.items() if not k.startswith("MD2_")}
+    runs = {"clean": base, "knobs": dict(base, **KNOBS), "tuned": dict(base, MD2_TUNING="1", **KNOBS)}
+    res = {}
+    for name, env in runs.items():
+        out = str(tmp_path / f"{name}.npy")
+        r = subprocess.run([sys.executable, "-c", _KNOB_CHILD, root, out], env=env, capture_output=True,
+                           text=True, timeout=200)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[name] = np.load(out)
+    assert np.array_equal(res["clean"], res["knobs"])
+    assert not np.array_equal(res["clean"], res["tuned"])

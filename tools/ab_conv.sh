@@ -1,4 +1,5 @@
 #!/bin/bash
+export MD2_TUNING=1   # kernel / planner knobs are honoured only with this (common.h tuning_knob)
 set -uo pipefail
 echo "=== w1"; MD2_W_V2=0 timeout -k 10 120 python3 tools/bench_conv.py || exit 1
 echo "=== w2"; timeout -k 10 120 python3 tools/bench_conv.py || exit 1

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Whole-step A/B of the split-K planners' minimum K chunks per split (MD2_PX_MINCH, MD2_W_MINCH):
 # bench.py (B=12, 416x128) per setting, one JSON line each.
+export MD2_TUNING=1   # kernel / planner knobs are honoured only with this (common.h tuning_knob)
 set -o pipefail
 mkdir -p gpurun_out
 for cfg in "8 8" "4 8" "8 4" "4 4" "2 2" "8 8"; do

@@ -1,4 +1,5 @@
 #!/bin/bash
+export MD2_TUNING=1   # kernel / planner knobs are honoured only with this (common.h tuning_knob)
 set -uo pipefail
 for CFG in "5 1536" "4 1536" "3 1536" "0 768" "0 1536"; do
   set -- $CFG

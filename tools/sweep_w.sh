@@ -1,4 +1,5 @@
 #!/bin/bash
+export MD2_TUNING=1   # kernel / planner knobs are honoured only with this (common.h tuning_knob)
 set -uo pipefail
 for CFG in "-1 512" "0 1024" "2 512" "2 1024" "2 2048" "3 1024" "1 1024"; do
   set -- $CFG

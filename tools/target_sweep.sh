@@ -1,6 +1,7 @@
 #!/bin/bash
 # Split-K block-target sweep of the conv planner (MD2_PX_TARGET for fwd/dgrad, MD2_W_TARGET /
 # MD2_W64_TARGET for wgrad): one per-layer table per setting under gpurun_out/sweep/.
+export MD2_TUNING=1   # kernel / planner knobs are honoured only with this (common.h tuning_knob)
 set -uo pipefail
 mkdir -p gpurun_out/sweep
 for t in ${PX_TARGETS:-}; do
