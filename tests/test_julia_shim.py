@@ -7,7 +7,10 @@ can be checked without it:
   * every Julia struct that mirrors a C struct (ModelCfg, LossCfg, LossOut, WarpCfg, ConvDesc)
     has the same field sequence, element counts and byte layout as the typedef in include/md2.h;
   * every ccall's argument-type tuple has as many entries as the C prototype has parameters;
-  * the rrules cover the op-level pullbacks the shim exposes."""
+  * the rrules cover the op-level pullbacks the shim exposes;
+  * train_loss keeps the reference's return convention (src/training.jl:36,71-77): a host scalar
+    loss and host visualisation arrays, and its pullback's θ tangent is an array in m.θ's own
+    layout reached through ``m.θ`` (Flux.params / implicit-gradient callers, scripts/script.jl:84-86)."""
 import ctypes
 import os
 import re
@@ -143,8 +146,42 @@ def test_ccalls_match_header_and_library(sources):
 
 def test_rrules_cover_the_op_level_pullbacks(sources):
     jl, _ = sources
-    for op in ("train_loss", "SSIM", "Backproject", "Project", "grid_sample_border", "smooth_loss",
+    for op in ("_train_loss", "SSIM", "Backproject", "Project", "grid_sample_border", "smooth_loss",
                "warp_photometric", "so3_compose"):
         assert re.search(r"ChainRulesCore\.rrule\((?:::typeof\()?\(?\w*::?%s" % op, jl) or \
             re.search(r"ChainRulesCore\.rrule\(\w+::%s" % op, jl) or \
             re.search(r"ChainRulesCore\.rrule\(::typeof\(%s\)" % op, jl), op
+
+
+def _function_body(jl, header_regex):
+    m = re.search(header_regex, jl)
+    assert m, header_regex
+    depth, i = 1, m.end()
+    # Julia blocks: count function/if/for/while/let/begin/do ... end pairs crudely by keywords
+    for tok in re.finditer(r"\b(function|if|for|while|let|begin|do|try)\b|\bend\b", jl[i:]):
+        depth += -1 if tok.group(0) == "end" else 1
+        if depth == 0:
+            return jl[m.start():i + tok.end()]
+    raise AssertionError("unbalanced " + header_regex)
+
+
+def test_train_loss_return_convention(sources):
+    jl, _ = sources
+    # train_loss passes m.θ through traced code, so Zygote's implicit Params see the gradient
+    assert re.search(r"train_loss\(m::HIPModel[^)]*\)\s*=\s*\n?\s*_train_loss\(m, m\.θ,", jl)
+    body = _function_body(jl, r"function _train_loss\(m::HIPModel")
+    # the loss is a host scalar: copied out of the device vector before returning
+    assert re.search(r"l = Array\(loss\)\[1\]", body)
+    assert "return (l, nothing, nothing, nothing)" in body
+    # visualisation outputs are host arrays (cpu(...) in the reference)
+    ret = body[body.rindex("return (l,"):]
+    assert ret.count("Array(") == 4, ret
+    # the rrule: θ tangent = a fresh array in θ's layout (the library gradient), m itself untangented
+    rr = _function_body(jl, r"function ChainRulesCore\.rrule\(::typeof\(_train_loss\)")
+    assert re.search(r"return \(NoTangent\(\), NoTangent\(\), copy\(m\.∇θ\),", rr)
+    assert "Tangent{HIPModel}" not in rr
+    # Flux.params(m) is exactly [m.θ]
+    assert re.search(r"Flux\.@functor HIPModel \(θ,\)", jl)
+    assert re.search(r"Flux\.trainable\(m::HIPModel\) = \(θ = m\.θ,\)", jl)
+    # after an update of θ outside the library the packed weights are refreshed before use
+    assert "m.packed || repack!(m)" in body
