@@ -290,6 +290,9 @@ typedef struct md2_model_cfg {
   int automasking;                      /* Params.automasking                                */
   int target, src0, src1;               /* 0-based frame ids in 0:2 (TrainCache target_id /
                                            source_ids minus 1)                                */
+  int embedding_levels;                 /* DepthDecoder(; embedding_levels): 0 = mono mode (the
+                                           measured step); 2L+1 (21) = MPI mode, model.jl:31-55 */
+  int num_bins;                         /* MPI mode: disparity planes per sample (model.jl:31)  */
 } md2_model_cfg;
 
 typedef struct md2_model md2_model;
@@ -370,7 +373,17 @@ int md2_model_train_step_dp(md2_model* m, md2_comm* comm, const float* x, const 
                             float* adam_m, float* adam_v, float lr, float beta1, float beta2,
                             float eps, int step, float* loss, void* stream);
 
-/* device pointers of the last forward: disparities per level and poses [2*batch][6] */
+/* MPI mode (embedding_levels > 0; src/model.jl:31-55, batch 1): the decoder runs on
+ * num_bins*batch plane images, image n*num_bins + p = cat(target features of sample n,
+ * repeat(embed(bins[n][p]), h, w)); the loss treats the planes as the batch, each warped with
+ * its sample's poses against its sample's frames (the broadcast of src/training.jl:42-56); the
+ * backward block-sums the planes' feature gradients (_repeat pullback, src/repeat.jl:44-53).
+ * bins [batch][num_bins] (device or host): uniformly_sample_disparity_from_linspace_bins's draw
+ * (src/model.jl:17-21, CUDA.rand there), used by every following forward until set again. */
+int md2_model_set_disparity_bins(md2_model* m, const float* bins, void* stream);
+
+/* device pointers of the last forward: disparities per level ([batch*num_bins][h][w] in MPI
+ * mode) and poses [2*batch][6] */
 int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose);
 /* The five encoder stage outputs of the last forward (device memory owned by the model):
  * feat[k] = [3n frame-major images][c[k]][h[k]][w[k]] (image l*n + i = frame l of sample i). */

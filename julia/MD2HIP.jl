@@ -39,6 +39,7 @@ struct ModelCfg                                        # md2_model_cfg
     min_depth::Cfloat; max_depth::Cfloat; disparity_smoothness::Cfloat
     scales::NTuple{5,Cfloat}; automasking::Cint
     target::Cint; src0::Cint; src1::Cint
+    embedding_levels::Cint; num_bins::Cint
 end
 
 # Params / TrainCache of src/Monodepth.jl:37-60 -> md2_model_cfg

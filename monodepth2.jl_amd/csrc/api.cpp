@@ -327,11 +327,13 @@ static ArchCfg to_arch(const md2_model_cfg* c) {
   a.in_ch = c->in_channels;
   a.nlevels = c->n_levels;
   for (int i = 0; i < MAX_SCALES; ++i) a.levels[i] = c->scale_levels[i];
+  a.emb = c->embedding_levels;
   return a;
 }
 
 int md2_arch_param_count(const md2_model_cfg* cfg, long long* n_entries, long long* n_elems) {
   MD2_CHECK_ARG(cfg != nullptr, "cfg");
+  MD2_CHECK_ARG(cfg->embedding_levels >= 0, "embedding_levels >= 0");
   MD2_CHECK_ARG(cfg->arch == 18 || cfg->arch == 34 || cfg->arch == 50, "arch 18/34/50");
   MD2_TRY(check_scale_levels(to_arch(cfg)));
   const auto t = build_param_table(to_arch(cfg));
@@ -375,6 +377,7 @@ int md2_model_create(const md2_model_cfg* c, float* params, float* grads, md2_mo
   mc.target = c->target;
   mc.src0 = c->src0;
   mc.src1 = c->src1;
+  mc.num_bins = c->num_bins;
   Model* m = nullptr;
   MD2_TRY(model_create(mc, params, grads, &m));
   *out = new md2_model{m};
@@ -469,6 +472,11 @@ int md2_model_profile_records(md2_model* m, int max, double* ms, double* work, i
                               int tag_len, int* count) {
   MD2_CHECK_ARG(m, "model");
   return model_profile_records(m->impl, max, ms, work, cat, tags, tag_len, count);
+}
+
+int md2_model_set_disparity_bins(md2_model* m, const float* bins, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_set_bins(m->impl, bins, (hipStream_t)stream);
 }
 
 int md2_model_outputs(md2_model* m, const float** disp, int* w, int* h, const float** pose) {

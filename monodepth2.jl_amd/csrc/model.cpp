@@ -138,8 +138,8 @@ ArchSpec build_spec(const ArchCfg& a) {
   // DepthDecoder(; encoder_channels, scale_levels, embedding_levels=0) src/depth_decoder.jl:26-50
   S.depth_begin = S.total;
   const int dec[5] = {256, 128, 64, 32, 16};
-  int encr[5];
-  for (int i = 0; i < 5; ++i) encr[i] = S.enc_ch[4 - i];
+  int encr[5];   // + embedding_levels in MPI mode (src/depth_decoder.jl:32)
+  for (int i = 0; i < 5; ++i) encr[i] = S.enc_ch[4 - i] + a.emb;
   const int in_ch[5] = {encr[0], dec[0], dec[1], dec[2], dec[3]};
   const int skip[5] = {encr[1], encr[2], encr[3], encr[4], 0};
   int bstart = 1;
@@ -241,6 +241,15 @@ class Model {
   int featC[5] = {}, featH[5] = {}, featW[5] = {};
   std::vector<DecBranch> br;
   float* d_skip[4] = {};
+  // MPI mode (src/model.jl:31-55): E embedding channels, NP planes per sample, ND = N*NP decoder
+  // images (image n*NP + p).  emb_in[f] = cat(repeat(target features f, P), repeat(embed(bins),
+  // h, w)) is the decoder's input / skip of level f; d_emb[f] its gradient, block-summed over the
+  // planes into the target features' gradient (the _repeat pullback, src/repeat.jl:44-53).
+  int E = 0, NP = 1, ND = 0;
+  float* emb_in[5] = {};
+  float* d_emb[5] = {};
+  float* bins = nullptr;                        // [N][P]
+  float *pose_rep = nullptr, *d_pose_rep = nullptr, *amask_rep = nullptr;
   // pose
   RConv sq, p1, p2, p3;
   float *sqo = nullptr, *pc1 = nullptr, *pc2 = nullptr, *means = nullptr, *pose = nullptr;
@@ -340,6 +349,9 @@ class Model {
     spec = build_spec(A);
     N = cfg.N;
     B = 3 * N;
+    E = A.emb;
+    NP = E > 0 ? cfg.num_bins : 1;
+    ND = N * NP;
     const int C = A.in_ch;
     size_t wsn = 0, scratch = 0;
     long bnmax = 0;
@@ -413,7 +425,13 @@ class Model {
       feat[si + 1] = cur;
       featC[si + 1] = cC; featH[si + 1] = cH; featW[si + 1] = cW;
     }
-    // ---- depth decoder (N target images)
+    // ---- depth decoder (ND = N target images, times P planes in MPI mode)
+    if (E > 0) {
+      MD2_TRY(alloc(&bins, (long)N * NP));
+      MD2_HIP(hipMemset(bins, 0, sizeof(float) * N * NP));
+      MD2_TRY(alloc(&emb_in[4], (long)ND * (featC[4] + E) * featH[4] * featW[4]));
+      MD2_TRY(alloc(&d_emb[4], (long)ND * (featC[4] + E) * featH[4] * featW[4]));
+    }
     int h = featH[4], w = featW[4];
     for (auto& bs : spec.branches) {
       DecBranch d;
@@ -421,20 +439,20 @@ class Model {
       d.h = h;
       d.w = w;
       MD2_TRY(make_conv(d.c1, bs.c1, h, w, true, wsn));
-      need_ws(d.c1, N, wsn, true);
+      need_ws(d.c1, ND, wsn, true);
       MD2_TRY(make_conv(d.c2, bs.c2, 2 * h, 2 * w, true, wsn));
-      need_ws(d.c2, N, wsn, true);
-      MD2_TRY(alloc(&d.o1, (long)N * bs.cout * h * w));
-      MD2_TRY(alloc(&d.up, (long)N * bs.cout * 4 * h * w));
-      MD2_TRY(alloc(&d.o2, (long)N * bs.cout * 4 * h * w));
-      MD2_TRY(alloc(&d.d_o2, (long)N * bs.cout * 4 * h * w));
-      track((long)N * (bs.cout + bs.cskip) * 4 * h * w);
+      need_ws(d.c2, ND, wsn, true);
+      MD2_TRY(alloc(&d.o1, (long)ND * bs.cout * h * w));
+      MD2_TRY(alloc(&d.up, (long)ND * bs.cout * 4 * h * w));
+      MD2_TRY(alloc(&d.o2, (long)ND * bs.cout * 4 * h * w));
+      MD2_TRY(alloc(&d.d_o2, (long)ND * bs.cout * 4 * h * w));
+      track((long)ND * (bs.cout + bs.cskip) * 4 * h * w);
       if (bs.head >= 0) {
         d.head = bs.head;
         MD2_TRY(make_conv(d.hc, spec.heads[bs.head], 2 * h, 2 * w, true, wsn));
-        need_ws(d.hc, N, wsn, true);
-        MD2_TRY(alloc(&d.disp, (long)N * 4 * h * w));
-        MD2_TRY(alloc(&d.d_head, (long)N * 4 * h * w));
+        need_ws(d.hc, ND, wsn, true);
+        MD2_TRY(alloc(&d.disp, (long)ND * 4 * h * w));
+        MD2_TRY(alloc(&d.d_head, (long)ND * 4 * h * w));
       }
       if (bs.bid <= 4) {
         const int fi = 4 - bs.bid;
@@ -443,6 +461,10 @@ class Model {
           return MD2_EINVAL;
         }
         MD2_TRY(alloc(&d_skip[fi], (long)N * featC[fi] * 4 * h * w));
+        if (E > 0) {
+          MD2_TRY(alloc(&emb_in[fi], (long)ND * (featC[fi] + E) * 4 * h * w));
+          MD2_TRY(alloc(&d_emb[fi], (long)ND * (featC[fi] + E) * 4 * h * w));
+        }
       }
       h *= 2;
       w *= 2;
@@ -503,8 +525,17 @@ class Model {
       q = (double*)v;
       bnws.partials = q;
     }
-    // ---- loss tail (src/training.jl:21-78)
-    tail.N = N;
+    // ---- loss tail (src/training.jl:21-78).  MPI mode: the ND plane disparities are the batch
+    // (training.jl:42-51 reshapes depth to (1, W*H, dn) with dn = num_bins*N); the poses and the
+    // frames of the one sample broadcast over its planes (Project's batched_mul of the 3x3x1 R,
+    // grid_sample and SSIM against the N = 1 images): x sample stride 0, poses / automask
+    // repeated per plane
+    if (E > 0) {
+      MD2_TRY(alloc(&pose_rep, 2L * ND * 6));
+      MD2_TRY(alloc(&d_pose_rep, 2L * ND * 6));
+      if (cfg.automask) MD2_TRY(alloc(&amask_rep, (long)ND * cfg.H * cfg.W));
+    }
+    tail.N = ND;
     tail.C = C;
     tail.W = cfg.W;
     tail.H = cfg.H;
@@ -524,7 +555,7 @@ class Model {
     tail.min_depth = cfg.min_depth;
     tail.max_depth = cfg.max_depth;
     tail.x_frame_stride = (long)C * cfg.H * cfg.W;
-    tail.x_sample_stride = 3 * tail.x_frame_stride;
+    tail.x_sample_stride = E > 0 ? 0 : 3 * tail.x_frame_stride;   // MPI: N == 1, planes share x
     tail.target = cfg.target;
     tail.src0 = cfg.src0;
     tail.src1 = cfg.src1;
@@ -759,9 +790,26 @@ class Model {
   }
 
   // ---- depth decoder over nimg images whose features start at image offset `img0`
+  // MPI mode: the decoder inputs of all levels from the target features of the last forward
+  int mpi_embed(int nimg, int img0, hipStream_t st) {
+    for (int fi = 0; fi < 5; ++fi)
+      if (emb_in[fi]) {
+        const long hw = (long)featH[fi] * featW[fi];
+        MD2_TRY(mpi_embed_features(feat[fi] + (long)img0 * featC[fi] * hw, (long)featC[fi] * hw, nimg,
+                                   featC[fi], featH[fi], featW[fi], bins, NP, (E - 1) / 2, emb_in[fi], st));
+      }
+    return MD2_OK;
+  }
+
   int decoder_fwd(int nimg, int img0, hipStream_t st) {
     const float* x = feat[4] + (long)img0 * featC[4] * featH[4] * featW[4];
     int C = featC[4];
+    if (E > 0) {                       // decoder batch: nimg * P plane images
+      MD2_TRY(mpi_embed(nimg, img0, st));
+      x = emb_in[4];
+      C = featC[4] + E;
+      nimg *= NP;
+    }
     for (auto& d : br) {
       const long hw = (long)d.h * d.w, hw2 = 4 * hw;
       const int co = d.b.cout;
@@ -770,8 +818,13 @@ class Model {
       TensorIn in = tin(d.up, co, hw2);
       if (d.b.cskip > 0) {
         const int fi = 4 - d.b.bid;
-        in.p1 = feat[fi] + (long)img0 * featC[fi] * hw2;
-        in.bs1 = (long)featC[fi] * hw2;
+        if (E > 0) {
+          in.p1 = emb_in[fi];
+          in.bs1 = (long)(featC[fi] + E) * hw2;
+        } else {
+          in.p1 = feat[fi] + (long)img0 * featC[fi] * hw2;
+          in.bs1 = (long)featC[fi] * hw2;
+        }
       }
       MD2_TRY(conv_f(d.c2, nimg, in, d.o2, co * hw2, ACT_ELU, 0, st));
       if (d.head >= 0) MD2_TRY(conv_f(d.hc, nimg, tin(d.o2, co, hw2), d.disp, hw2, ACT_SIGMOID, 0, st));
@@ -822,7 +875,7 @@ class Model {
       }
     o.loss = loss ? loss : loss_buf;
     o.terms = terms;
-    o.d_pose = d_pose;
+    o.d_pose = E > 0 ? d_pose_rep : d_pose;
     hipEvent_t pev[2 * MAX_SCALES] = {};
     if (prof) {
       for (int k = 0; k < 2; ++k) pev[k] = ev();
@@ -835,11 +888,22 @@ class Model {
                               tail.src1, N, cfg.arch.in_ch, cfg.H, cfg.W, amask, st));
       automask = amask;
     }
-    MD2_TRY(loss_tail_run(tail, disps, pose, x, cfg.automask ? automask : nullptr, 1.f, o, tail_ws, st));
+    const float* tail_pose = pose;
+    if (E > 0) {
+      // every plane of a sample warps with that sample's poses and is compared with its frames
+      MD2_TRY(repeat_rows(pose, 2L * N, 6, NP, pose_rep, st));
+      tail_pose = pose_rep;
+      if (cfg.automask) {
+        MD2_TRY(repeat_rows(automask, N, cfg.H * cfg.W, NP, amask_rep, st));
+        automask = amask_rep;
+      }
+    }
+    MD2_TRY(loss_tail_run(tail, disps, tail_pose, x, cfg.automask ? automask : nullptr, 1.f, o, tail_ws, st));
+    if (E > 0) MD2_TRY(repeat_rows_adjoint(d_pose_rep, 2L * N, 6, NP, d_pose, st));
     if (prof) {
       // one launch for all scales; algorithmic bytes per full-res pixel and scale:
       // disparity 4 + target 4C + two sources 8C + d_disp 4
-      const double bytes = (double)tail.nscales * N * cfg.H * cfg.W * (8.0 + 12.0 * cfg.arch.in_ch);
+      const double bytes = (double)tail.nscales * ND * cfg.H * cfg.W * (8.0 + 12.0 * cfg.arch.in_ch);
       recs.push_back({pev[0], pev[1], PROF_PHOTO, bytes, "photometric (all scales)"});
     }
     return MD2_OK;
@@ -1034,34 +1098,51 @@ class Model {
     MD2_TRY(act_bias(sqo, d_sq, d_sq, B, 256, hw4, ACT_RELU, st));
     float* d_f4 = stages[3].back().d_out;
     MD2_TRY(conv_wd(sq, B, tin(feat[4], featC[4], hw4), d_sq, d_f4, (long)featC[4] * hw4, 0, st));
-    // ---- DepthDecoder backward (reverse branch order)
+    // ---- DepthDecoder backward (reverse branch order), over ND decoder images
     const int nb = (int)br.size();
     for (int i = nb - 1; i >= 0; --i) {
       DecBranch& d = br[i];
       const long hw = (long)d.h * d.w, hw2 = 4 * hw;
       const int co = d.b.cout;
       if (d.head >= 0) {
-        MD2_TRY(conv_wd(d.hc, N, tin(d.o2, co, hw2), d.d_head, d.d_o2, co * hw2, i < nb - 1 ? 1 : 0, st));
+        MD2_TRY(conv_wd(d.hc, ND, tin(d.o2, co, hw2), d.d_head, d.d_o2, co * hw2, i < nb - 1 ? 1 : 0, st));
       }
-      MD2_TRY(act_bias(d.o2, d.d_o2, DPRE, N, co, hw2, ACT_ELU, st));
+      MD2_TRY(act_bias(d.o2, d.d_o2, DPRE, ND, co, hw2, ACT_ELU, st));
       TensorIn in = tin(d.up, co, hw2);
       float* dskip = nullptr;
       long skip_bs = 0;
       if (d.b.cskip > 0) {
         const int fi = 4 - d.b.bid;
-        in.p1 = feat[fi] + (long)T0 * featC[fi] * hw2;
-        in.bs1 = (long)featC[fi] * hw2;
-        dskip = d_skip[fi];
-        skip_bs = (long)featC[fi] * hw2;
+        if (E > 0) {
+          in.p1 = emb_in[fi];
+          in.bs1 = (long)(featC[fi] + E) * hw2;
+          dskip = d_emb[fi];
+          skip_bs = (long)(featC[fi] + E) * hw2;
+        } else {
+          in.p1 = feat[fi] + (long)T0 * featC[fi] * hw2;
+          in.bs1 = (long)featC[fi] * hw2;
+          dskip = d_skip[fi];
+          skip_bs = (long)featC[fi] * hw2;
+        }
       }
-      MD2_TRY(conv_wd(d.c2, N, in, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
-      MD2_TRY(upsample2_bwd(DUP, N, co, d.h, d.w, DO1, st));
-      MD2_TRY(act_bias(d.o1, DO1, DO1, N, co, hw, ACT_ELU, st));
+      MD2_TRY(conv_wd(d.c2, ND, in, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
+      if (E > 0 && d.b.cskip > 0) {
+        // _repeat pullback: the skip gradient of the target features = sum over the planes
+        const int fi = 4 - d.b.bid;
+        MD2_TRY(plane_sum(d_emb[fi], N, NP, featC[fi] + E, featC[fi], hw2, d_skip[fi], 0, st));
+      }
+      MD2_TRY(upsample2_bwd(DUP, ND, co, d.h, d.w, DO1, st));
+      MD2_TRY(act_bias(d.o1, DO1, DO1, ND, co, hw, ACT_ELU, st));
       const float* xin;
       int cin;
       float* dx;
       int acc;
-      if (i == 0) {
+      if (i == 0 && E > 0) {
+        cin = featC[4] + E;
+        xin = emb_in[4];
+        dx = d_emb[4];
+        acc = 0;
+      } else if (i == 0) {
         cin = featC[4];
         xin = feat[4] + (long)T0 * cin * hw;
         dx = d_f4 + (long)T0 * cin * hw;
@@ -1072,7 +1153,9 @@ class Model {
         dx = br[i - 1].d_o2;
         acc = 0;
       }
-      MD2_TRY(conv_wd(d.c1, N, tin(xin, cin, hw), DO1, dx, (long)cin * hw, acc, st));
+      MD2_TRY(conv_wd(d.c1, ND, tin(xin, cin, hw), DO1, dx, (long)cin * hw, acc, st));
+      if (i == 0 && E > 0)
+        MD2_TRY(plane_sum(d_emb[4], N, NP, cin, featC[4], hw, d_f4 + (long)T0 * featC[4] * hw, 1, st));
     }
     return MD2_OK;
   }
@@ -1147,6 +1230,17 @@ int model_create(const ModelCfg& cfg, float* params, float* grads, Model** out) 
   MD2_CHECK_ARG(cfg.target >= 0 && cfg.target < 3 && cfg.src0 >= 0 && cfg.src0 < 3 && cfg.src1 >= 0 &&
                     cfg.src1 < 3, "target / source ids must be frames of the triplet (1-based 1:3)");
   MD2_TRY(check_scale_levels(cfg.arch));
+  MD2_CHECK_ARG(cfg.arch.emb == 0 || (cfg.arch.emb > 0 && cfg.arch.emb % 2 == 1),
+                "embedding_levels must be 0 or 2L+1 (x, sin, cos of L octaves)");
+  if (cfg.arch.emb > 0) {
+    MD2_CHECK_ARG(cfg.num_bins >= 1, "num_bins >= 1");
+    if (cfg.N != 1) {
+      // src/training.jl:42-56 with planes merged into the batch is shape-consistent only for one
+      // sample: Project / grid_sample broadcast the N = 1 poses and frames
+      set_error("MPI mode (embedding_levels > 0) trains one sample per step (batch must be 1)");
+      return MD2_ENOTSUP;
+    }
+  }
   Model* m = new Model();
   m->cfg = cfg;
   m->params = params;
@@ -1367,6 +1461,12 @@ int model_features(Model* m, const float** feat, int* c, int* h, int* w) {
 
 int model_eval_disparity(Model* m, const float* x, int n, float** disp_out, hipStream_t st) {
   MD2_CHECK_ARG(m && x && n >= 1 && n <= m->N, "eval_disparity: 1 <= n <= batch");
+  if (m->E > 0) {
+    // src/model.jl:63 runs the decoder on the bare encoder features, which an
+    // embedding_levels > 0 DepthDecoder cannot take (defect D4)
+    set_error("eval_disparity: the MPI-mode DepthDecoder (embedding_levels > 0) has no mono input");
+    return MD2_ENOTSUP;
+  }
   // inference reuses the executor's activation buffers: a pending train forward is gone, and a
   // backward after this must fail instead of differentiating the eval batch
   m->cur_x = nullptr;
@@ -1434,8 +1534,18 @@ int model_scale_loss_cotangent(Model* m, float dloss, hipStream_t st) {
   MD2_CHECK_ARG(m && m->cur_x, "loss cotangent before forward");
   if (dloss == 1.f) return MD2_OK;
   for (auto& d : m->br)
-    if (d.head >= 0) MD2_TRY(scale_inplace(d.d_head, (long)m->N * 4 * d.h * d.w, dloss, st));
+    if (d.head >= 0) MD2_TRY(scale_inplace(d.d_head, (long)m->ND * 4 * d.h * d.w, dloss, st));
   return scale_inplace(m->d_pose, 2L * m->N * 6, dloss, st);
+}
+
+int model_set_bins(Model* m, const float* bins, hipStream_t st) {
+  MD2_CHECK_ARG(m && bins, "set_bins args");
+  if (m->E == 0) {
+    set_error("set_bins: the model is not in MPI mode (embedding_levels = 0)");
+    return MD2_ESTATE;
+  }
+  MD2_HIP(hipMemcpyAsync(m->bins, bins, sizeof(float) * m->N * m->NP, hipMemcpyDefault, st));
+  return MD2_OK;
 }
 
 long model_param_count(Model* m) { return m ? m->spec.total : 0; }

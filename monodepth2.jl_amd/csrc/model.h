@@ -16,6 +16,7 @@ struct ArchCfg {
   int in_ch = 3;
   int nlevels = 4;
   int levels[MAX_SCALES] = {2, 3, 4, 5};
+  int emb = 0;             // DepthDecoder embedding_levels (0: mono mode; 21: MPI mode)
 };
 
 struct ParamEntry {
@@ -37,6 +38,7 @@ struct ModelCfg {
   float scales[MAX_SCALES] = {0.125f, 0.25f, 0.5f, 1.f};
   int automask = 0;
   int target = 1, src0 = 0, src1 = 2;   // 0-based frame ids, L = 3
+  int num_bins = 32;       // MPI mode (arch.emb > 0): disparity planes per sample
 };
 
 // profiling categories (HIP events around each launch, md2_model_profile_read)
@@ -67,6 +69,8 @@ int model_repack(Model* m, hipStream_t st);   // after the parameters changed
 // forward + loss + backward + ADAM(0.9, 0.999, 1e-8) replayed as one captured hipGraph
 int model_train_step_graph(Model* m, const float* x, const float* auto_loss, float* adam_m,
                            float* adam_v, float lr, int step, float* loss, hipStream_t st);
+// MPI mode: the disparity bins [N][num_bins] of the next forwards (device; copied)
+int model_set_bins(Model* m, const float* bins, hipStream_t st);
 // outputs of the last forward
 int model_outputs(Model* m, const float** disp, int* dw, int* dh, const float** pose);
 // the five encoder stage outputs of the last forward: [3N frame-major images][c][h][w]

@@ -107,6 +107,13 @@ int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStr
 // embed(bins[b][p])[e] broadcast over h x w (e < 2L+1: x, sin(2^i x), cos(2^i x))
 int mpi_embed_features(const float* feat, long sample_stride, int N, int C, int h, int w,
                        const float* bins, int P, int L, float* out, hipStream_t st);
+// the _repeat pullback (src/repeat.jl:44-53): out[b][c] (+)= sum_p in[b*P + p][c] for c < C of the
+// Cin channels per image (hw % 4 == 0)
+int plane_sum(const float* in, int N, int P, int Cin, int C, long hw, float* out, int accumulate,
+              hipStream_t st);
+// dst[r*P + p][:] = src[r][:] for a [rows][cols] matrix, and its adjoint dst[r] = sum_p src[r*P + p]
+int repeat_rows(const float* src, long rows, int cols, int P, float* dst, hipStream_t st);
+int repeat_rows_adjoint(const float* src, long rows, int cols, int P, float* dst, hipStream_t st);
 // channel concatenation cat(a, b; dims=3) of [N][ca][hw] and [N][cb][hw]
 int concat_channels(const float* a, int ca, const float* b, int cb, int N, long hw, float* out,
                     hipStream_t st);

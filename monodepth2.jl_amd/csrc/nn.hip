@@ -1063,6 +1063,89 @@ __global__ __launch_bounds__(256) void mpi_embed_kernel(const float* __restrict_
   out[i] = v;
 }
 
+// The _repeat pullback over the plane axis (src/repeat.jl:44-53, block sum): for the first C of
+// the Cin channels of every decoder input image, out[b][c][q] (+)= sum_p in[b*P + p][c][q], in the
+// fixed order p = 0..P-1 (the embedding channels c >= C get no gradient: embed is
+// @non_differentiable, src/model.jl:15).  4 pixels per thread.
+__global__ __launch_bounds__(256) void plane_sum_kernel(const float* __restrict__ in, int P, int Cin,
+                                                        int C, int hw4, float* __restrict__ out,
+                                                        int acc, long n4) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int q = (int)(i % hw4);
+  const long t = i / hw4;
+  const int c = (int)(t % C);
+  const long b = t / C;
+  const long pstride = (long)Cin * hw4;
+  const float4* src = reinterpret_cast<const float4*>(in) + ((b * P) * Cin + c) * (long)hw4 + q;
+  float4 s = src[0];
+  for (int p = 1; p < P; ++p) {
+    const float4 v = src[(long)p * pstride];
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  float4* dst = reinterpret_cast<float4*>(out) + i;
+  if (acc) {
+    const float4 o = *dst;
+    s.x += o.x;
+    s.y += o.y;
+    s.z += o.z;
+    s.w += o.w;
+  }
+  *dst = s;
+}
+
+int plane_sum(const float* in, int N, int P, int Cin, int C, long hw, float* out, int accumulate,
+              hipStream_t st) {
+  if (hw % 4 != 0) {
+    set_error("plane_sum: h*w must be a multiple of 4");
+    return MD2_EINVAL;
+  }
+  const long n4 = (long)N * C * (hw / 4);
+  MD2_TRY(check_u31(4 * n4));
+  hipLaunchKernelGGL(plane_sum_kernel, dim3(cdiv(n4, 256)), dim3(256), 0, st, in, P, Cin, C,
+                     (int)(hw / 4), out, accumulate, n4);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
+// rows of a [R][cols] matrix repeated P times (row r -> rows r*P .. r*P+P-1) and the adjoint sum
+__global__ __launch_bounds__(256) void repeat_rows_kernel(const float* __restrict__ src, int cols,
+                                                          int P, float* __restrict__ dst, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long row = i / cols;
+  dst[i] = src[(row / P) * cols + (i - row * cols)];
+}
+__global__ __launch_bounds__(256) void repeat_rows_adj_kernel(const float* __restrict__ src, int cols,
+                                                              int P, float* __restrict__ dst, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long row = i / cols, col = i - row * cols;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += src[(row * P + p) * cols + col];
+  dst[i] = s;
+}
+
+int repeat_rows(const float* src, long rows, int cols, int P, float* dst, hipStream_t st) {
+  const long n = rows * P * cols;
+  MD2_TRY(check_u31(n));
+  if (n == 0) return MD2_OK;
+  hipLaunchKernelGGL(repeat_rows_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, src, cols, P, dst, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+int repeat_rows_adjoint(const float* src, long rows, int cols, int P, float* dst, hipStream_t st) {
+  const long n = rows * cols;
+  MD2_TRY(check_u31(n * P));
+  if (n == 0) return MD2_OK;
+  hipLaunchKernelGGL(repeat_rows_adj_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, src, cols, P, dst, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 int mpi_embed_features(const float* feat, long sample_stride, int N, int C, int h, int w,
                        const float* bins, int P, int L, float* out, hipStream_t st) {
   const long n = (long)N * P * (C + 2 * L + 1) * h * w;

@@ -55,6 +55,7 @@ class ModelCfg(C.Structure):
         ("min_depth", C.c_float), ("max_depth", C.c_float), ("disparity_smoothness", C.c_float),
         ("scales", C.c_float * MAX_SCALES),
         ("automasking", C.c_int), ("target", C.c_int), ("src0", C.c_int), ("src1", C.c_int),
+        ("embedding_levels", C.c_int), ("num_bins", C.c_int),
     ]
 
 
@@ -113,6 +114,7 @@ _SIGS = {
     "md2_model_get_params": (C.c_int, [P, P, P]),
     "md2_model_get_grads": (C.c_int, [P, P, P]),
     "md2_model_loss_cotangent": (C.c_int, [P, C.c_float, P]),
+    "md2_model_set_disparity_bins": (C.c_int, [P, P, P]),
     "md2_model_outputs": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.POINTER(C.c_void_p)]),
     "md2_model_eval_disparity": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_void_p), P]),

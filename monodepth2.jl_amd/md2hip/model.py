@@ -41,16 +41,16 @@ ResNet = ResidualNetwork
 
 
 class DepthDecoder:
-    """``DepthDecoder(; encoder_channels, scale_levels, embedding_levels=21)``."""
+    """``DepthDecoder(; encoder_channels, scale_levels, embedding_levels=21)``.  embedding_levels
+    = 0 is the mono decoder of the measured step; 2L+1 (the reference's default 21) is the MPI-mode
+    decoder whose inputs carry the plane embedding (src/model.jl:31-55, trained at batch 1)."""
 
     def __init__(self, *, encoder_channels, scale_levels, embedding_levels: int = 21):
         levels = list(scale_levels)
         if len(levels) > 5 or min(levels) < 1 or max(levels) > 5:   # src/depth_decoder.jl:27-29
             raise ValueError("`scale_levels` should be at most of length 5 and have values in [1, 5] range.")
-        if embedding_levels != 0:
-            # defects D2/D4 (SURVEY.md section 0): the MPI-embedding decoder is forward-only upstream
-            raise NotImplementedError("the HIP train step runs the mono DepthDecoder (embedding_levels=0); "
-                                      "MPI mode (forward only, as upstream): md2hip.MPIDepthDecoder + md2hip.mpi_forward")
+        if embedding_levels < 0 or (embedding_levels and embedding_levels % 2 != 1):
+            raise ValueError("embedding_levels must be 0 or 2L+1 (x, sin, cos of L octaves; src/model.jl:4-15)")
         if any(b <= a for a, b in zip(levels, levels[1:])):
             # the reference builds an empty branch here: a duplicate head for a repeated level, a
             # channel mismatch at run time for a decreasing one (library: MD2_ENOTSUP)
@@ -75,9 +75,10 @@ class Pose:
 
 
 def _cfg(arch, in_ch, levels, batch=1, width=64, height=64, cache: Optional[TrainCache] = None,
-         params: Optional[Params] = None) -> ModelCfg:
+         params: Optional[Params] = None, embedding_levels: int = 0, num_bins: int = 32) -> ModelCfg:
     c = ModelCfg()
     c.arch, c.in_channels, c.batch, c.width, c.height = arch, in_ch, batch, width, height
+    c.embedding_levels, c.num_bins = embedding_levels, num_bins
     c.n_levels = len(levels)
     for i, l in enumerate(levels):
         c.scale_levels[i] = l
@@ -103,9 +104,9 @@ def _cfg(arch, in_ch, levels, batch=1, width=64, height=64, cache: Optional[Trai
     return c
 
 
-def param_table(arch=18, in_channels=3, scale_levels=(2, 3, 4, 5)):
+def param_table(arch=18, in_channels=3, scale_levels=(2, 3, 4, 5), embedding_levels=0):
     """[(name, shape, offset)] of the flat parameter vector (host-only library query)."""
-    cfg = _cfg(arch, in_channels, scale_levels)
+    cfg = _cfg(arch, in_channels, scale_levels, embedding_levels=embedding_levels)
     ne, nel = C.c_longlong(), C.c_longlong()
     check(lib().md2_arch_param_count(C.byref(cfg), C.byref(ne), C.byref(nel)), "md2_arch_param_count")
     out = []
@@ -142,11 +143,14 @@ def flux_init(table, total, seed=42):
 class _Executor:
     """One libmd2hip model instance (activations/workspace) for a fixed problem size."""
 
-    def __init__(self, model: "Model", batch, height, width, cache: TrainCache, params: Params):
+    def __init__(self, model: "Model", batch, height, width, cache: TrainCache, params: Params,
+                 num_bins: int = 32):
         self.model = model
         self.batch, self.height, self.width = batch, height, width
+        self.emb = model.depth_decoder.embedding_levels
+        self.num_bins = num_bins if self.emb else 1
         cfg = _cfg(model.encoder.depth, model.encoder.in_channels, model.depth_decoder.scale_levels,
-                   batch, width, height, cache, params)
+                   batch, width, height, cache, params, self.emb, num_bins)
         h = C.c_void_p()
         check(lib().md2_model_create(C.byref(cfg), ptr(model.flat), ptr(model.grad), C.byref(h)),
               "md2_model_create")
@@ -202,6 +206,17 @@ class _Executor:
                  self.PROF_CATS[cat[i]] if cat[i] < len(self.PROF_CATS) else str(cat[i]), ms[i], work[i])
                 for i in range(count.value)]
 
+    def set_bins(self, bins):
+        """MPI mode: the disparity bins [batch, num_bins] of the next forwards (the reference's
+        ``uniformly_sample_disparity_from_linspace_bins`` draw, src/model.jl:17-21)."""
+        import torch
+        b = bins.to(self.model.device, torch.float32).contiguous()
+        if tuple(b.shape) != (self.batch, self.num_bins):
+            raise ValueError(f"bins must be [{self.batch}, {self.num_bins}]")
+        check(lib().md2_model_set_disparity_bins(self.handle, ptr(b), stream_of(self.model.device)),
+              "md2_model_set_disparity_bins")
+        self._bins = b                       # the copy is async: keep the source alive
+
     def forward_loss(self, x, auto_loss=None, loss=None, terms=None):
         import torch
         loss = loss if loss is not None else torch.empty(1, dtype=torch.float32, device=x.device)
@@ -256,7 +271,8 @@ class _Executor:
         h = (C.c_int * 5)()
         pp = C.c_void_p()
         check(lib().md2_model_outputs(self.handle, dptr, w, h, C.byref(pp)), "md2_model_outputs")
-        disps = [_wrap(dptr[i], (self.batch, 1, h[i], w[i]), self.model.device) for i in range(nl)]
+        disps = [_wrap(dptr[i], (self.batch * self.num_bins, 1, h[i], w[i]), self.model.device)
+                 for i in range(nl)]
         pose = _wrap(pp.value, (2 * self.batch, 6), self.model.device)
         return disps, pose
 
@@ -300,7 +316,8 @@ class Model:
             raise ValueError("PoseDecoder channels must equal encoder.stages[end]")
         self.encoder, self.depth_decoder, self.pose_decoder = encoder, depth_decoder, pose_decoder
         self.device = torch.device(device)
-        self.table, self.numel = param_table(encoder.depth, encoder.in_channels, depth_decoder.scale_levels)
+        self.table, self.numel = param_table(encoder.depth, encoder.in_channels, depth_decoder.scale_levels,
+                                             depth_decoder.embedding_levels)
         self.flat = flux_init(self.table, self.numel, seed).to(self.device, torch.float32)
         self.grad = torch.zeros_like(self.flat)
         self._ex: Dict[tuple, _Executor] = {}
@@ -328,16 +345,17 @@ class Model:
             if ex is self._last:
                 self._last = None
 
-    def executor(self, x_shape, cache: TrainCache, params: Params) -> _Executor:
+    def executor(self, x_shape, cache: TrainCache, params: Params, num_bins: int = 32) -> _Executor:
         N, L, Cc, H, W = x_shape
         if L != 3 or Cc != self.encoder.in_channels:
             raise ValueError("x must be [N, 3, in_channels, H, W]")
         if (W, H) != tuple(params.target_size):
             raise ValueError("x size != Params.target_size")
+        nb = num_bins if self.depth_decoder.embedding_levels else 1
         key = (N, H, W, tuple(np.asarray(cache.K).reshape(-1)), tuple(cache.scales), params.min_depth,
-               params.max_depth, params.disparity_smoothness, params.automasking)
+               params.max_depth, params.disparity_smoothness, params.automasking, nb)
         if key not in self._ex:
-            self._ex[key] = _Executor(self, N, H, W, cache, params)
+            self._ex[key] = _Executor(self, N, H, W, cache, params, nb)
         self._last = self._ex[key]
         self._last.sync()
         return self._last
@@ -357,32 +375,53 @@ class Model:
         cache = TrainCache(K=K, invK=iK)
         params = Params(target_size=(W, H), batch_size=N, automasking=False)
         key = (N, H, W, tuple(np.asarray(cache.K).reshape(-1)), tuple(cache.scales), params.min_depth,
-               params.max_depth, params.disparity_smoothness, params.automasking)
+               params.max_depth, params.disparity_smoothness, params.automasking, 1)
         key = key + ("eval",) if key in self._ex else key          # that one has a pending forward
         ex = self._ex[key] = _Executor(self, N, H, W, cache, params)   # leaves _last (training) alone
         return ex
 
     def __call__(self, x, source_ids=(1, 3), target_id=2, cache: Optional[TrainCache] = None,
-                 params: Optional[Params] = None):
-        """Mono-mode forward (src/model.jl:31-55): returns (disparities, [Pose, Pose])."""
+                 params: Optional[Params] = None, num_bins: int = 32, bins=None):
+        """``(m::Model)(x, source_ids, target_id; num_bins=32)`` (src/model.jl:31-55): returns
+        (disparities, [Pose, Pose]).  MPI mode (embedding_levels > 0): disparities of the
+        N*num_bins plane images; ``bins`` [N, num_bins] (default: a fresh uniform draw, as the
+        reference's CUDA.rand)."""
         N, L, Cc, H, W = x.shape
         if cache is None:
             K, iK = depth10k_intrinsics(W, H)
             cache = TrainCache(K=K, invK=iK, target_id=target_id, source_ids=tuple(source_ids))
         if params is None:
             params = Params(target_size=(W, H), batch_size=N, automasking=False)
-        ex = self.executor(tuple(x.shape), cache, params)
+        ex = self.executor(tuple(x.shape), cache, params, num_bins)
+        if ex.emb:
+            ex.set_bins(disparity_bins(N, num_bins, device=self.device) if bins is None else bins)
         ex.forward_loss(x, None)
         disps, pose = ex.outputs()
         return disps, [Pose(pose[s * N:(s + 1) * N, 0:3], pose[s * N:(s + 1) * N, 3:6]) for s in range(2)]
 
 
+def disparity_bins(batch: int, num_bins: int, u=None, device="cuda", near=1.0, far=0.001):
+    """``uniformly_sample_disparity_from_linspace_bins(num_bins, batch_size)`` (src/model.jl:17-21):
+    bins[n][p] = linspace(near, far, num_bins+1)[p] + u[n][p] * interval, u ~ U[0,1) (drawn here
+    when not given -- the reference draws with CUDA.rand, defect D3) -> float32 [batch, num_bins]."""
+    import torch
+    if u is None:
+        u = torch.rand(batch, num_bins, dtype=torch.float64)
+    edges = torch.linspace(near, far, num_bins + 1, dtype=torch.float64)[:-1]
+    interval = float(edges[1] - edges[0])
+    return (edges.unsqueeze(0) + u.double().cpu() * interval).float().to(device).contiguous()
+
+
 def train_loss(model: Model, x, auto_loss, cache: TrainCache, params: Params,
-               do_visualization: bool = False):
+               do_visualization: bool = False, num_bins: int = 32, bins=None):
     """``train_loss(model, x, auto_loss, cache, params, do_visualization)`` (src/training.jl:21).
     Runs the forward and the fused loss-tail pullback; call ``gradient(model)`` for the rest of
-    the backward.  Returns (loss, vis_disparity, vis_warped, vis_loss)."""
-    ex = model.executor(tuple(x.shape), cache, params)
+    the backward.  Returns (loss, vis_disparity, vis_warped, vis_loss).  MPI mode (the model's
+    DepthDecoder has embedding_levels > 0; batch 1): ``num_bins`` planes, ``bins`` [1, num_bins]
+    (default: a fresh draw of md2hip.disparity_bins)."""
+    ex = model.executor(tuple(x.shape), cache, params, num_bins)
+    if ex.emb:
+        ex.set_bins(disparity_bins(x.shape[0], num_bins, device=x.device) if bins is None else bins)
     loss = ex.forward_loss(x, auto_loss)
     if not do_visualization:
         return loss, None, None, None
@@ -390,10 +429,19 @@ def train_loss(model: Model, x, auto_loss, cache: TrainCache, params: Params,
     # loss of the last scale, on the host.  Recomputed from the model outputs by the loss-tail
     # kernels (forward only, after the step's own forward; the gradient state is untouched).
     disps, pose = ex.outputs()
-    N = x.shape[0]
+    N, nb = x.shape[0], ex.num_bins
     poses = [(pose[s * N:(s + 1) * N, 0:3], pose[s * N:(s + 1) * N, 3:6]) for s in range(2)]
-    vis = loss_tail(disps, poses, x.contiguous(), auto_loss, cache, params, grads=False,
-                    visualize=True)
+    xv = x.contiguous()
+    if nb > 1:           # MPI: every plane against its sample's frames and poses
+        xv = xv.repeat_interleave(nb, 0).contiguous()
+        poses = [(r.repeat_interleave(nb, 0).contiguous(), t.repeat_interleave(nb, 0).contiguous())
+                 for r, t in poses]
+        if auto_loss is not None:
+            auto_loss = auto_loss.repeat_interleave(nb, 0).contiguous()
+    vis = loss_tail(disps, poses, xv, auto_loss, cache,
+                    Params(target_size=params.target_size, batch_size=N * nb, min_depth=params.min_depth,
+                           max_depth=params.max_depth, disparity_smoothness=params.disparity_smoothness,
+                           automasking=params.automasking), grads=False, visualize=True)
     return (loss, disps[-1].cpu(), [w.cpu() for w in vis["vis_warped"].unbind(0)],
             vis["vis_loss"][-1].unsqueeze(1).cpu())
 
@@ -478,6 +526,9 @@ def eval_disparity(model: Model, x, cache: Optional[TrainCache] = None):
     N, Cc, H, W = x.shape
     if Cc != model.encoder.in_channels:
         raise ValueError("x must be [N, in_channels, H, W]")
+    if model.depth_decoder.embedding_levels:
+        raise NotImplementedError("eval_disparity (src/model.jl:63) feeds the bare encoder features, which "
+                                  "an embedding_levels > 0 DepthDecoder cannot take (defect D4)")
     ex = model.eval_executor(N, H, W)
     dptr = (C.c_void_p * 5)()
     ex.forwarded = False            # the library discards any pending forward of this executor

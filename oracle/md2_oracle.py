@@ -568,13 +568,21 @@ def pose_decoder(P, fa, fb, tag="pose"):
     return pose[:, 0:3], pose[:, 3:6]
 
 
-def model_forward(P, x, source_ids=(1, 3), target_id=2, arch=18, scale_levels=(2, 3, 4, 5)):
-    """Mono-mode ``(m::Model)(x, source_ids, target_id)`` (src/model.jl:31-55 without the MPI
-    embedding; defect D2 makes MPI mode shape-inconsistent for B>1).  x [N,L,C,H,W]."""
+def model_forward(P, x, source_ids=(1, 3), target_id=2, arch=18, scale_levels=(2, 3, 4, 5),
+                  mpi_bins=None, embedding_levels=21):
+    """``(m::Model)(x, source_ids, target_id)`` (src/model.jl:31-55).  x [N,L,C,H,W].
+    Mono mode (``mpi_bins`` None): the DepthDecoder on the target frame's features.
+    MPI mode: ``mpi_bins`` [N, num_bins] are the disparity bins (the CURAND draw injected, D3);
+    the decoder runs on the N*num_bins plane images (image n*num_bins + p) of
+    cat(repeat(target features), repeat(embed(bins), w, h)) (:39-50).  The poses are the same."""
     N, L, C, H, W = x.shape
     feats = resnet_stages(P, x.reshape(N * L, C, H, W), arch)
     feats = [f.reshape(N, L, *f.shape[1:]) for f in feats]
-    disps = depth_decoder(P, [f[:, target_id - 1] for f in feats], scale_levels)
+    if mpi_bins is None:
+        disps = depth_decoder(P, [f[:, target_id - 1] for f in feats], scale_levels)
+    else:
+        disps = depth_decoder(P, mpi_decoder_inputs([f[:, target_id - 1] for f in feats], mpi_bins,
+                                                    embedding_levels), scale_levels)
     poses = []
     for j, i in enumerate(source_ids):                             # eval_poses, src/model.jl:57-70
         if i < target_id:
@@ -617,6 +625,48 @@ def disparity_bins(num_bins: int, u: torch.Tensor, near=1.0, far=0.001):
     edges = torch.linspace(near, far, num_bins + 1, dtype=u.dtype)[:-1]
     interval = edges[1] - edges[0]
     return edges.unsqueeze(0) + u * interval
+
+
+def mpi_decoder_inputs(target_feats, bins, embedding_levels=21):
+    """src/model.jl:39-50: per feature level cat(repeat(f[target], num_bins), repeat(embed(bins),
+    w, h)) with planes merged into the batch -> [N*num_bins, c+E, h, w].  ``repeat`` is the
+    gist's _repeat (src/repeat.jl:3-17); autograd's adjoint of the expand is its block-sum
+    pullback (:44-53)."""
+    N, nb = bins.shape
+    emb = embed(bins, (embedding_levels - 1) // 2)                  # [N, nb, E]
+    out = []
+    for f in target_feats:
+        c, h, w = f.shape[1:]
+        rep = f.unsqueeze(1).expand(N, nb, c, h, w)
+        e = emb[:, :, :, None, None].expand(N, nb, emb.shape[-1], h, w)
+        out.append(torch.cat([rep, e], 2).reshape(N * nb, c + emb.shape[-1], h, w))
+    return out
+
+
+def mpi_train_loss(P, x, bins, auto_loss, cache: TrainCache, params: Params, arch=18,
+                   scale_levels=(2, 3, 4, 5), embedding_levels=21, forced_sel=None,
+                   forced_cells=None):
+    """``train_loss`` (src/training.jl:21-78) on the MPI-mode Model at batch 1 -- the case the
+    reference's shapes admit: the N*num_bins plane disparities are the batch of
+    every per-scale op (:42-51: dn = num_bins), and the ONE sample's poses (R 3x3x1, t 3x1x1)
+    and frames (x[:, :, :, id, :] with N = 1) broadcast over the planes in Project's batched_mul,
+    grid_sample and SSIM.  (grid_sample's batch broadcast is the reading under which the whole
+    body is consistent: NNlib's CPU kernel would sample plane 1 only, NNlibCUDA's would index the
+    1-image input with the plane index.)  Restated as loss_from_outputs over N*num_bins samples
+    with each sample's frames and poses repeated per plane."""
+    N = x.shape[0]
+    nb = bins.shape[1]
+    disps, poses = model_forward(P, x, cache.source_ids, cache.target_id, arch, scale_levels,
+                                 mpi_bins=bins, embedding_levels=embedding_levels)
+    x_rep = x.repeat_interleave(nb, 0)
+    poses_rep = [(r.repeat_interleave(nb, 0), t.repeat_interleave(nb, 0)) for r, t in poses]
+    am = auto_loss.repeat_interleave(nb, 0) if auto_loss is not None else None
+    par = Params(target_size=params.target_size, batch_size=N * nb, min_depth=params.min_depth,
+                 max_depth=params.max_depth, disparity_smoothness=params.disparity_smoothness,
+                 automasking=params.automasking)
+    loss = loss_from_outputs(disps, poses_rep, x_rep, am, cache, par, forced_sel=forced_sel,
+                             forced_cells=forced_cells)
+    return loss, disps, poses
 
 
 def mpi_model_forward(P, x, u, source_ids=(1, 3), target_id=2, arch=18, scale_levels=(2, 3, 4, 5),

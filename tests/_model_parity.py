@@ -35,47 +35,55 @@ def _sources(strict, sources):
     return sources if sources is not None else ("ramp" if strict else "texture")
 
 
+def mpi_bins(N, num_bins, seed=3):
+    """Seeded disparity bins (the reference's CUDA.rand draw injected, defect D3)."""
+    u = torch.rand(N, num_bins, generator=torch.Generator().manual_seed(seed), dtype=torch.float64)
+    return md2hip.disparity_bins(N, num_bins, u=u, device="cpu")
+
+
 def run(N=2, C=3, H=64, W=128, arch=18, strict=True, seed=7, automasking=False, levels=(2, 3, 4, 5),
-        target_id=2, source_ids=(1, 3), sources=None):
+        target_id=2, source_ids=(1, 3), sources=None, num_bins=0):
+    """num_bins > 0: the MPI-mode Model (DepthDecoder(embedding_levels=21), batch 1, num_bins
+    planes) against O.mpi_train_loss."""
     sources = _sources(strict, sources)
     x = inputs(N, C, H, W, sources, seed)
     K, invK = D.intrinsics(W, H)
+    emb = 21 if num_bins else 0
     enc = md2hip.ResNet(arch, in_channels=C)
     model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=list(levels),
-                                                  embedding_levels=0),
+                                                  embedding_levels=emb),
                          md2hip.PoseDecoder(enc.stages[-1]), seed=42)
     scales = tuple(DEFAULT_SCALES[l] for l in levels)
     cache = md2hip.TrainCache(K=K.numpy(), invK=invK.numpy(), target_id=target_id,
                               source_ids=tuple(source_ids), scales=scales)
     params = md2hip.Params(target_size=(W, H), batch_size=N, automasking=automasking)
     xg = x.float().cuda().contiguous()
-    loss, *_ = md2hip.train_loss(model, xg, None, cache, params)
+    bins = mpi_bins(N, num_bins) if num_bins else None
+    nb = max(1, num_bins)
+    loss, *_ = md2hip.train_loss(model, xg, None, cache, params, num_bins=nb,
+                                 bins=bins.cuda() if bins is not None else None)
     disps, pose = model._last.outputs()
     md2hip.gradient(model)
-    poses_g = [(pose[:N, :3].contiguous(), pose[:N, 3:].contiguous()),
-               (pose[N:, :3].contiguous(), pose[N:, 3:].contiguous())]
-    tail = md2hip.loss_tail([d.contiguous() for d in disps], poses_g, xg, None, cache, params, visualize=True)
+    # the loss tail again at the GPU's outputs, recording its argmin and bilinear cells (planes of
+    # an MPI sample broadcast its frames and poses: repeated here)
+    xt = xg.repeat_interleave(nb, 0).contiguous() if nb > 1 else xg
+    poses_g = [(pose[s * N:(s + 1) * N, :3].repeat_interleave(nb, 0).contiguous(),
+                pose[s * N:(s + 1) * N, 3:].repeat_interleave(nb, 0).contiguous()) for s in range(2)]
+    params_t = md2hip.Params(target_size=(W, H), batch_size=N * nb, automasking=automasking)
+    am_t = None
+    if automasking:
+        from md2hip.primitives import automasking_loss
+        am_t = automasking_loss(xg, target_id, tuple(source_ids)).repeat_interleave(nb, 0).contiguous()
+    tail = md2hip.loss_tail([d.contiguous() for d in disps], poses_g, xt, am_t, cache, params_t, visualize=True)
     torch.cuda.synchronize()
     g = {"loss": loss.item(), "tail_loss": tail["loss"].item(), "disps": [d.cpu() for d in disps],
          "pose": pose.cpu(), "grad": model.grad.cpu(), "sel": tail["vis_sel"].cpu(),
          "cells": tail["vis_cell"].cpu(), "flat": model.flat.detach().double().cpu(),
-         "x": x, "sources": sources, "automasking": automasking}
+         "x": x, "sources": sources, "automasking": automasking, "bins": bins,
+         "levels": tuple(levels), "target_id": target_id, "source_ids": tuple(source_ids)}
     g["decisions"] = gpu_decisions(model, N, arch, target_id=target_id, source_ids=source_ids)
-    spec = O.param_spec(arch, C, tuple(levels))
-    flat = model.flat.detach().double().cpu().clone().requires_grad_(True)
-    P = O.unflatten(flat, spec)
-    with O.forced_decisions(g["decisions"]):
-        d_o, p_o = O.model_forward(P, x, source_ids, target_id, arch=arch, scale_levels=tuple(levels))
-    cache_o = O.TrainCache(K=K, invK=invK, target_id=target_id, source_ids=tuple(source_ids), scales=scales)
-    par_o = O.Params(target_size=(W, H), batch_size=N, automasking=automasking)
-    # the GPU's argmin (-1 = automask) as an index into [auto_loss?, source 0, source 1]
-    forced = [g["sel"][s].unsqueeze(1).long() + (1 if automasking else 0) for s in range(len(levels))]
-    auto_o = O.automasking_loss(x, x[:, target_id - 1], source_ids) if automasking else None
-    loss_o = O.loss_from_outputs(d_o, p_o, x, auto_o, cache_o, par_o, forced_sel=forced,
-                                 forced_cells=g["cells"])
-    loss_o.backward()
-    o = {"loss": loss_o.item(), "disps": [d.detach() for d in d_o],
-         "pose": torch.cat([torch.cat([r, t], 1) for r, t in p_o], 0).detach(), "grad": flat.grad}
+    grad_o, fwd_o, loss_o, spec = _oracle_grad(g, torch.float64, arch, levels, target_id, source_ids)
+    o = {"loss": loss_o, "disps": fwd_o[0], "pose": fwd_o[1], "grad": grad_o}
     return g, o, per_tensor(spec, g["grad"], o["grad"])
 
 
@@ -124,13 +132,17 @@ def _oracle_grad(g, dt, arch, levels, target_id, source_ids, perturb=None, seed=
     x = g["x"]
     N, L, C, H, W = x.shape
     K, invK = D.intrinsics(W, H)
-    spec = O.param_spec(arch, C, tuple(levels))
+    bins = g.get("bins")
+    emb = 21 if bins is not None else 0
+    nb = bins.shape[1] if bins is not None else 1
+    spec = O.param_spec(arch, C, tuple(levels), embedding_levels=emb)
     scales = tuple(DEFAULT_SCALES[l] for l in levels)
     f = g["flat"].to(dt).clone().requires_grad_(True)
     P = O.unflatten(f, spec)
     with O.forced_decisions(g["decisions"]):
         d_o, p_o = O.model_forward(P, x.to(dt), source_ids, target_id, arch=arch,
-                                   scale_levels=tuple(levels))
+                                   scale_levels=tuple(levels),
+                                   mpi_bins=None if bins is None else bins.to(dt), embedding_levels=emb)
     if perturb:
         gen = torch.Generator().manual_seed(seed)
         noise = lambda t: t + (t * perturb * torch.randn(t.shape, generator=gen, dtype=t.dtype)).detach()
@@ -139,10 +151,13 @@ def _oracle_grad(g, dt, arch, levels, target_id, source_ids, perturb=None, seed=
     cache_o = O.TrainCache(K=K.to(dt), invK=invK.to(dt), target_id=target_id,
                            source_ids=tuple(source_ids), scales=scales)
     am = g["automasking"]
-    par_o = O.Params(target_size=(W, H), batch_size=N, automasking=am)
+    # MPI: the planes are the loss batch, each with its sample's frames and poses (O.mpi_train_loss)
+    xt = x.to(dt).repeat_interleave(nb, 0) if nb > 1 else x.to(dt)
+    pt = [(r.repeat_interleave(nb, 0), t.repeat_interleave(nb, 0)) for r, t in p_o] if nb > 1 else p_o
+    par_o = O.Params(target_size=(W, H), batch_size=N * nb, automasking=am)
     forced = [s.unsqueeze(1).long() + (1 if am else 0) for s in g["sel"]]
-    auto_o = O.automasking_loss(x.to(dt), x[:, target_id - 1].to(dt), source_ids) if am else None
-    lo = O.loss_from_outputs(d_o, p_o, x.to(dt), auto_o, cache_o, par_o, forced_sel=forced,
+    auto_o = O.automasking_loss(xt, xt[:, target_id - 1], source_ids) if am else None
+    lo = O.loss_from_outputs(d_o, pt, xt, auto_o, cache_o, par_o, forced_sel=forced,
                              forced_cells=g["cells"])
     lo.backward()
     fwd = ([d.detach().double() for d in d_o], torch.cat([torch.cat([r, t], 1) for r, t in p_o], 0).detach().double())
@@ -166,7 +181,8 @@ def oracle_bounds(g, o=None, eps=2.0 ** -23, arch=18, levels=(2, 3, 4, 5), targe
         g64, f64, l64, spec = _oracle_grad(g, torch.float64, **kw)
     else:
         g64, f64, l64 = o["grad"].double(), (o["disps"], o["pose"]), o["loss"]
-        spec = O.param_spec(arch, g["x"].shape[2], tuple(levels))
+        spec = O.param_spec(arch, g["x"].shape[2], tuple(levels),
+                            embedding_levels=21 if g.get("bins") is not None else 0)
     g32, f32, l32, _ = _oracle_grad(g, torch.float32, **kw)
     floor = per_tensor(spec, g32, g64)
     for s_, (a, b) in enumerate(zip(f32[0], f64[0])):

@@ -83,3 +83,27 @@ def test_general_frame_ids_accepted():
         c = _cfg(18, 3, (1, 3, 5), cache=md2hip.TrainCache(K=K, invK=iK, target_id=t, source_ids=s,
                                                            scales=(0.0625, 0.25, 1.0)))
         assert (c.target, c.src0, c.src1) == (t - 1, s[0] - 1, s[1] - 1)
+
+
+@pytest.mark.parametrize("arch,levels", [(18, (2, 3, 4, 5)), (50, (2, 3, 4, 5)), (18, (1, 3, 5))])
+def test_mpi_param_table_matches_oracle(arch, levels):
+    """MPI mode: DepthDecoder(; embedding_levels=21) widens every decoder input by the embedding
+    (src/depth_decoder.jl:32) -- the library table equals the oracle's spec."""
+    import md2hip
+    table, total = md2hip.param_table(arch, 3, levels, embedding_levels=21)
+    spec = O.param_spec(arch, 3, levels, embedding_levels=21)
+    assert [(t[0], tuple(t[1])) for t in table] == [(s[0], tuple(s[1])) for s in spec]
+    d = {t[0]: tuple(t[1]) for t in table}
+    enc = O.encoder_stage_channels(arch)
+    assert d["depth.branch1.c1.weight"][1] == enc[4] + 21
+
+
+def test_disparity_bins_definition():
+    """uniformly_sample_disparity_from_linspace_bins (src/model.jl:17-21)."""
+    import md2hip
+    u = torch.tensor([[0.0, 0.5, 0.25]], dtype=torch.float64)
+    b = md2hip.disparity_bins(1, 3, u=u, device="cpu")
+    edges = np.linspace(1.0, 0.001, 4)[:-1]
+    iv = edges[1] - edges[0]
+    np.testing.assert_allclose(b.numpy()[0], (edges + u.numpy()[0] * iv).astype(np.float32))
+    assert b.dtype == torch.float32

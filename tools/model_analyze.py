@@ -15,7 +15,7 @@ from oracle import md2_oracle as O  # noqa: E402
 from tests import _data as D  # noqa: E402
 from tests._model_parity import per_tensor  # noqa: E402
 
-torch.set_num_threads(os.cpu_count())
+torch.set_num_threads(min(16, os.cpu_count()))
 dmp = torch.load(sys.argv[1], weights_only=False)
 g = dmp["g"]
 x = g["x"]
