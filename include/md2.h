@@ -180,6 +180,22 @@ int md2_warp_photometric_bwd(const md2_warp_cfg* cfg, const float* disp, const f
                              const float* x, const float* automask, const float* d_loss,
                              float* d_disp, float* d_Rt, void* workspace, void* stream);
 
+/* Data pipeline, host code: PNG files (8-bit, non-interlaced gray / RGB / RGBA)
+ * decoded on `threads` host threads straight into the uint8 batch layout (lossless: the bytes of
+ * FileIO/PNGFiles' N0f8 arrays).
+ * md2_load_triplets_u8   Depth10k (src/dtk.jl:29-46): file i = three frames side by side (3W x H
+ *                        RGB) -> out [n][3][3][H][W], frame j = columns [jW, (j+1)W); flip[i]
+ *                        (NULL = none) mirrors every frame of sample i (FlipX).
+ * md2_load_kitti_u8      KittyDataset (src/kitty.jl:45-61): paths[3i+k] = frame k of sample i
+ *                        (8-bit gray) -> out [n][3][1][h][w], each imresize'd to (h, w) and kept
+ *                        N0f8 (md2hip/data.py imresize), then flipped if flip[i].
+ * Host pointers; errors name the offending file. */
+int md2_png_info(const char* path, int* width, int* height, int* channels);
+int md2_load_triplets_u8(const char* const* paths, int n, int width, int height,
+                         const unsigned char* flip, unsigned char* out, int threads);
+int md2_load_kitti_u8(const char* const* paths, int n, int height, int width,
+                      const unsigned char* flip, unsigned char* out, int threads);
+
 /* Data pipeline: N0f8 images -> Float32, out[i] = Float32(in[i]) / 255f0, the
  * `Float32.(channelview(x))` of src/dtk.jl:45 / src/kitty.jl:58 -- batches cross PCIe as bytes.
  * in 4-byte aligned, out 16-byte aligned. */

@@ -102,7 +102,8 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
   const int KT = rows + 4;        // P1 rows y0-2 .. y0+rows+1
 
   const __amdgpu_buffer_rsrc_t rxs =
-      make_rsrc(a.x + (long)n * a.x_sample_stride, (uint32_t)(a.x_sample_stride * 4));
+      make_rsrc(a.x + (long)n * a.x_sample_stride, (uint32_t)(3 * a.x_frame_stride * 4));   // the 3 frames
+                                                   // (sample stride 0: MPI planes share them)
   const int dw = sc.dw, dh = sc.dh;
   const __amdgpu_buffer_rsrc_t rdsp =
       make_rsrc(sc.disp + (long)n * dw * dh, (uint32_t)dw * dh * 4u);

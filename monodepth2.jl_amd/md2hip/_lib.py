@@ -144,6 +144,9 @@ _SIGS = {
     "md2_grid_sample_border_bwd": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                              P, P, P]),
     "md2_unorm8_to_float": (C.c_int, [P, P, C.c_longlong, P]),
+    "md2_png_info": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "md2_load_triplets_u8": (C.c_int, [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_int, P, P, C.c_int]),
+    "md2_load_kitti_u8": (C.c_int, [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_int, P, P, C.c_int]),
     "md2_smooth_loss_workspace_size": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
     "md2_smooth_loss_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]),
     "md2_smooth_loss_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, P, P, P]),

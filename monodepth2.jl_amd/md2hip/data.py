@@ -122,6 +122,20 @@ class FlipX:
         return frames
 
 
+def _torch_from(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def _addr(a) -> int:
+    """Data pointer of a C-contiguous numpy array or CPU torch tensor."""
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"]
+        return a.ctypes.data
+    assert a.is_contiguous() and not a.is_cuda
+    return a.data_ptr()
+
+
 def intrinsics(fx: float, fy: float, cx: float, cy: float) -> np.ndarray:
     """``construct_intrinsic`` (src/kitty.jl:92-97)."""
     return np.array([[fx, 0.0, cx], [0.0, fy, cy], [0.0, 0.0, 1.0]])
@@ -137,6 +151,32 @@ class _Dataset:
         if self.augmentations is None:
             return frames
         return self.augmentations(frames, np.random.default_rng((seed, i)))
+
+    def _native_flips(self, idx, seed):
+        """The FlipX coins of samples ``idx`` (the same draws as _augment), or None when the
+        augmentations are not the natively supported ones (nothing or one FlipX)."""
+        a = self.augmentations
+        if a is None:
+            return np.zeros(len(idx), dtype=np.uint8)
+        if isinstance(a, FlipX):
+            return np.array([np.random.default_rng((seed, i)).random() < a.p for i in idx], dtype=np.uint8)
+        return None
+
+    def batch_u8(self, idx, seed: int = 0, threads: int = 8, out=None):
+        """Samples ``idx`` as one uint8 [n][3][C][H][W] array, decoded by the library's native
+        loader on ``threads`` host threads (md2_load_*_u8); the per-sample Python path when the
+        augmentations are not natively supported.  ``out``: a caller buffer (e.g. pinned)."""
+        w, h = self.resolution
+        if out is None:
+            out = np.empty((len(idx), 3, self.channels, h, w), dtype=np.uint8)
+        flips = self._native_flips(idx, seed)
+        if flips is None:
+            for k, i in enumerate(idx):
+                s = self.getobs_u8(i, seed)
+                out[k] = s if isinstance(out, np.ndarray) else _torch_from(s)
+            return out
+        self._native_load(idx, flips, out, threads)
+        return out
 
     def getobs(self, i: int, seed: int = 0) -> np.ndarray:
         return _unorm(self.getobs_u8(i, seed))
@@ -168,6 +208,13 @@ class Depth10k(_Dataset):
                              f"{img.shape[2]}x{img.shape[1]}")
         frames = [img[:, :, width * j:width * (j + 1)] for j in range(3)]
         return np.stack(self._augment(frames, i, seed), 0)
+
+    def _native_load(self, idx, flips, out, threads):
+        from ._lib import check, lib
+        paths = (C.c_char_p * len(idx))(*[os.path.join(self.dir, self.files[i]).encode() for i in idx])
+        w, h = self.resolution
+        check(lib().md2_load_triplets_u8(paths, len(idx), w, h, flips.ctypes.data_as(C.c_void_p),
+                                         C.c_void_p(_addr(out)), threads), "md2_load_triplets_u8")
 
     def getobs_u8(self, i: int, seed: int = 0) -> np.ndarray:
         """Sample ``i`` (0-based) as its N0f8 bytes: uint8 [3][3][H][W] (RGB only)."""
@@ -220,6 +267,15 @@ class KittyDataset(_Dataset):
     def __len__(self):
         return self.total_length
 
+    def _native_load(self, idx, flips, out, threads):
+        from ._lib import check, lib
+        files = [os.path.join(self.frames_dir, "%06d.png" % (i * len(self.frame_ids) + x - 1)).encode()
+                 for i in idx for x in self.frame_ids]
+        paths = (C.c_char_p * len(files))(*files)
+        w, h = self.resolution
+        check(lib().md2_load_kitti_u8(paths, len(idx), h, w, flips.ctypes.data_as(C.c_void_p),
+                                      C.c_void_p(_addr(out)), threads), "md2_load_kitti_u8")
+
     def getobs_u8(self, i: int, seed: int = 0) -> np.ndarray:
         """Sample ``i`` (0-based): frames 3i, 3i+1, 3i+2 (kitty.jl:47-61), each ``imresize``d to
         the target size and kept N0f8 -> uint8 [3][1][H][W]."""
@@ -260,6 +316,23 @@ class DChain:
         bid = next(b for b, edge in enumerate(self.bins) if i < edge)
         return self.datasets[bid].getobs_u8(i - (self.bins[bid - 1] if bid else 0), seed)
 
+    def batch_u8(self, idx, seed: int = 0, threads: int = 8, out=None):
+        """Per member dataset one native batch call, scattered back into ``idx`` order."""
+        w, h = self.resolution
+        if out is None:
+            out = np.empty((len(idx), 3, self.channels, h, w), dtype=np.uint8)
+        groups = {}
+        for k, i in enumerate(idx):
+            if not 0 <= i < len(self):
+                raise IndexError(i)
+            bid = next(b for b, edge in enumerate(self.bins) if i < edge)
+            groups.setdefault(bid, []).append((k, i - (self.bins[bid - 1] if bid else 0)))
+        for bid, items in groups.items():
+            sub = self.datasets[bid].batch_u8([li for _, li in items], seed, threads)
+            for (k, _), s in zip(items, sub):
+                out[k] = s if isinstance(out, np.ndarray) else _torch_from(s)
+        return out
+
     __getitem__ = getobs
 
 
@@ -271,14 +344,16 @@ class DataLoader:
     over ranks is identical for every GPU count.  Incomplete trailing batches are dropped
     (fixed-shape train step).  ``workers`` decode threads; one batch is prefetched and its
     host->device copy runs on a side stream while the previous batch trains.  ``bytes_h2d``
-    (default): N0f8 datasets are copied as uint8 and converted on the GPU."""
+    (default): N0f8 datasets are copied as uint8 and converted on the GPU.  ``native`` (default):
+    N0f8 datasets decode through the library's C++ PNG loader (md2_load_*_u8; GIL-free threads,
+    ``prefetch`` batches in flight, ``workers`` threads in all) into pinned memory."""
 
     def __init__(self, dataset, batch_size: int, *, shuffle: bool = True, seed: int = 0,
                  workers: int = 8, device=None, rank: int = 0, world: int = 1, prefetch: int = 2,
-                 bytes_h2d: bool = True):
+                 bytes_h2d: bool = True, native: bool = True):
         self.ds, self.batch_size, self.shuffle, self.seed = dataset, batch_size, shuffle, seed
         self.workers, self.rank, self.world, self.prefetch = workers, rank, world, prefetch
-        self.bytes_h2d = bytes_h2d
+        self.bytes_h2d, self.native = bytes_h2d, native
         self.device = device
         self.epoch = 0
 
@@ -309,21 +384,49 @@ class DataLoader:
         stop = threading.Event()
 
         use_u8 = on_gpu and self.bytes_h2d and getattr(self.ds, "u8", False)
+        native = self.native and getattr(self.ds, "u8", False) and hasattr(self.ds, "batch_u8")
         if use_u8:
             from ._lib import check, lib, ptr
             get = lambda i: self.ds.getobs_u8(i, seed=self.seed + epoch)
         else:
             get = lambda i: self.ds.getobs(i, seed=self.seed + epoch)
+        w_, h_ = self.ds.resolution
+        shape = (self.batch_size, 3, self.ds.channels, h_, w_)
+        jobs = max(1, min(self.prefetch, len(batches)))
+        per_call = max(1, self.workers // jobs)
+
+        def native_batch(idx):
+            # the library's PNG decoder on per_call host threads, straight into (pinned) memory
+            buf = torch.empty(shape, dtype=torch.uint8, pin_memory=on_gpu)
+            self.ds.batch_u8(idx, seed=self.seed + epoch, threads=per_call, out=buf)
+            return buf if use_u8 else torch.from_numpy(_unorm(buf.numpy()))
 
         def produce():
             try:
-                with ThreadPoolExecutor(self.workers) as pool:
-                    for idx in batches:
+                with ThreadPoolExecutor(jobs if native else self.workers) as pool:
+                    pending = []
+                    it = iter(batches)
+                    if native:               # `jobs` batches in flight, each decoded natively
+                        for idx in it:
+                            pending.append(pool.submit(native_batch, idx))
+                            if len(pending) >= jobs:
+                                break
+                    while pending or not native:
                         if stop.is_set():
                             return
-                        host = torch.from_numpy(np.stack(list(pool.map(get, idx)), 0))
+                        if native:
+                            host = pending.pop(0).result()
+                            nxt = next(it, None)
+                            if nxt is not None:
+                                pending.append(pool.submit(native_batch, nxt))
+                        else:
+                            idx = next(it, None)
+                            if idx is None:
+                                break
+                            host = torch.from_numpy(np.stack(list(pool.map(get, idx)), 0))
                         if on_gpu:
-                            host = host.pin_memory()
+                            if not host.is_pinned():
+                                host = host.pin_memory()
                             with torch.cuda.stream(stream):
                                 x = host.to(dev, non_blocking=True)
                                 if use_u8:          # N0f8 bytes -> Float32 on the GPU

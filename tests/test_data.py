@@ -194,3 +194,94 @@ def test_u8_samples_match_float_samples(dtk, tmp_path):
     u = kd.getobs_u8(0)
     assert u.dtype == np.uint8 and u.shape == (3, 1, 128, 416)
     np.testing.assert_array_equal(_unorm(u), kd[0])
+
+
+def _write_png_filters(path, img):
+    """A PNG whose rows cycle through all five filter types (None, Sub, Up, Average, Paeth), to
+    pin the native decoder's unfiltering (PIL picks its own filters)."""
+    import struct
+    import zlib
+    h, w = img.shape[:2]
+    c = 1 if img.ndim == 2 else img.shape[2]
+    a = img.reshape(h, w * c).astype(np.int64)
+    raw = bytearray()
+    for y in range(h):
+        ft = y % 5
+        cur, prev = a[y], (a[y - 1] if y else np.zeros_like(a[0]))
+        left = np.concatenate([np.zeros(c, np.int64), cur[:-c]])
+        ul = np.concatenate([np.zeros(c, np.int64), prev[:-c]])
+        if ft == 0:
+            f = cur
+        elif ft == 1:
+            f = cur - left
+        elif ft == 2:
+            f = cur - prev
+        elif ft == 3:
+            f = cur - (left + prev) // 2
+        else:
+            p = left + prev - ul
+            pa, pb, pc = np.abs(p - left), np.abs(p - prev), np.abs(p - ul)
+            pred = np.where((pa <= pb) & (pa <= pc), left, np.where(pb <= pc, prev, ul))
+            f = cur - pred
+        raw += bytes([ft]) + bytes((f % 256).astype(np.uint8))
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xffffffff)
+    ihdr = struct.pack(">IIBBBBB", w, h, 8, {1: 0, 3: 2, 4: 6}[c], 0, 0, 0)
+    idat = zlib.compress(bytes(raw), 6)
+    with open(path, "wb") as f:   # split IDAT in two chunks: the decoder must stream them
+        f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", idat[:len(idat) // 2]) +
+                chunk(b"IDAT", idat[len(idat) // 2:]) + chunk(b"IEND", b""))
+
+
+def test_native_png_decoder_all_filters(tmp_path):
+    """md2_load_triplets_u8 / md2_load_kitti_u8 decode every PNG row filter bit-exactly (PIL
+    agrees on the same files), RGBA drops alpha."""
+    import ctypes as C
+    import md2hip
+    from md2hip._lib import lib
+    rng = np.random.default_rng(7)
+    rgb = rng.integers(0, 256, (16, 3 * 20, 3), dtype=np.uint8)
+    _write_png_filters(str(tmp_path / "a.png"), rgb)
+    np.testing.assert_array_equal(np.asarray(Image.open(str(tmp_path / "a.png"))), rgb)
+    rgba = np.concatenate([rgb, rng.integers(0, 256, (16, 60, 1), dtype=np.uint8)], 2)
+    _write_png_filters(str(tmp_path / "b.png"), rgba)
+    out = np.empty((2, 3, 3, 16, 20), dtype=np.uint8)
+    paths = (C.c_char_p * 2)(str(tmp_path / "a.png").encode(), str(tmp_path / "b.png").encode())
+    flips = np.array([0, 1], dtype=np.uint8)
+    assert lib().md2_load_triplets_u8(paths, 2, 20, 16, flips.ctypes.data_as(C.c_void_p),
+                                      C.c_void_p(out.ctypes.data), 2) == 0
+    ref = np.stack([rgb[:, 20 * j:20 * (j + 1)].transpose(2, 0, 1) for j in range(3)], 0)
+    np.testing.assert_array_equal(out[0], ref)
+    np.testing.assert_array_equal(out[1], ref[..., ::-1])
+    w, h, c = C.c_int(), C.c_int(), C.c_int()
+    assert lib().md2_png_info(str(tmp_path / "b.png").encode(), C.byref(w), C.byref(h), C.byref(c)) == 0
+    assert (w.value, h.value, c.value) == (60, 16, 4)
+    # a bad file fails loudly with its name
+    (tmp_path / "bad.png").write_bytes(b"garbage")
+    paths = (C.c_char_p * 1)(str(tmp_path / "bad.png").encode())
+    assert lib().md2_load_triplets_u8(paths, 1, 20, 16, None, C.c_void_p(out.ctypes.data), 1) != 0
+    assert b"bad.png" in lib().md2_last_error()
+
+
+def test_native_batches_match_python_path(dtk, tmp_path):
+    """Depth10k + FlipX, KittyDataset (imresize 1241x376 -> 416x128 + FlipX) and a DChain of
+    both kinds: the native batch loader is bit-identical to the per-sample Python path, and the
+    host DataLoader (native, float) delivers the same samples as getobs."""
+    import md2hip
+    d, files = dtk
+    ds = md2hip.Depth10k(d, files, augmentations=md2hip.FlipX(0.5))
+    idx = [5, 0, 3, 2]
+    got = ds.batch_u8(idx, seed=4, threads=3)
+    np.testing.assert_array_equal(got, np.stack([ds.getobs_u8(i, seed=4) for i in idx]))
+    seq = tmp_path / "k" / "sequences" / "01" / "image_0"
+    seq.mkdir(parents=True)
+    (tmp_path / "k" / "sequences" / "01" / "calib.txt").write_text("P0: " + " ".join(["2.0"] * 12) + "\n")
+    rng = np.random.default_rng(8)
+    for k in range(9):
+        _write_png_filters(str(seq / ("%06d.png" % k)), rng.integers(0, 256, (376, 1241), dtype=np.uint8))
+    kd = md2hip.KittyDataset(str(tmp_path / "k"), "01", target_size=(128, 416), augmentations=md2hip.FlipX(0.5))
+    got = kd.batch_u8([2, 0, 1], seed=1, threads=4)
+    np.testing.assert_array_equal(got, np.stack([kd.getobs_u8(i, seed=1) for i in (2, 0, 1)]))
+    loader = md2hip.DataLoader(ds, 2, shuffle=True, seed=5, workers=4)
+    for b, x in zip(loader.batch_indices(0), loader):
+        np.testing.assert_array_equal(x.numpy(), np.stack([ds.getobs(i, seed=5) for i in b]))

@@ -7,8 +7,9 @@ run the exact kernels the bench times and compare them with the fp64 oracle, wit
 branch decision (ReLU masks, max-pool argmax, per-pixel argmin, bilinear cells and border clamps)
 imposed as in tests/_model_parity.py -- with affine-ramp sources, textured sources AND the
 bench's own uniform-random triplets.  Tolerances (tests/_model_parity.py check_step): forward 1e-5
-relative (disparities, poses), loss 1e-6, each gradient tensor within max(4 x the oracle's fp32
-floor, 4 x its 1-ulp forward sensitivity, 2e-5)."""
+relative (disparities, poses), loss 1e-6; each gradient tensor within max(4 x the backward's fp32
+floor, 2e-5) of the oracle evaluated at the GPU's own forward outputs, and within max(4 x the
+end-to-end fp32 floor, 2 x what the forward's rounding explains, 2e-5) of the plain oracle."""
 import json
 import os
 
@@ -26,8 +27,8 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "bench_first_loss.jso
 def _check_full_step(N, H, W, arch, sources):
     from tests._model_parity import check_step, oracle_bounds, run
     g, o, errs = run(N=N, H=H, W=W, arch=arch, sources=sources)
-    floor, sens = oracle_bounds(g, o, arch=arch)
-    return check_step(g, o, errs, floor, sens, label=f"R{arch} N={N} {W}x{H} {sources}")
+    b = oracle_bounds(g, o, arch=arch)
+    return check_step(g, o, errs, b, label=f"R{arch} N={N} {W}x{H} {sources}")
 
 
 @pytest.mark.timeout(400)

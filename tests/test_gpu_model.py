@@ -3,12 +3,13 @@
 Same flat parameters (Flux-default init, seed 42) and inputs; the GPU's per-pixel argmin is
 imposed on the oracle (see test_gpu_loss.py for why).  Tolerances:
   * forward: disparities / poses relative 1e-5, loss relative 1e-6;
-  * gradients, per parameter tensor: within max(4 x the fp32 noise floor, 4 x the 1-ulp forward
-    sensitivity, 2e-5) (tests/_model_parity.py grad_bounds): the floor is the error of the SAME
-    oracle evaluated in fp32 against fp64 -- the GPU must be as accurate as an fp32 evaluation of
-    the reference can be -- and the sensitivity is how far one fp32 ulp of noise on the
-    disparities / poses moves that gradient in the fp64 oracle (cancelling sums such as a head's
-    bias gradient);
+  * gradients, per parameter tensor (tests/_model_parity.py check_step):
+      - backward: within max(4 x its fp32 floor, 2e-5) of the fp64 oracle evaluated AT THE GPU's
+        own forward outputs (the exact gradient at the GPU's forward point);
+      - end to end: within max(4 x the oracle's fp32-vs-fp64 floor, 2 x what the forward's
+        rounding explains, 2e-5) of the plain fp64 oracle -- the forward's ~1e-6 rounding moves
+        cancelling-sum gradients (a head's bias: ~1e6 pixel gradients of both signs) by more than
+        the backward's own error, and that part is measured, not assumed;
   * every GPU branch decision is imposed on the oracle, including grid_sample's bilinear cells
     and border clamps, so textured and uniform-random source frames get the same bounds as
     kink-free affine ramps."""
@@ -30,8 +31,8 @@ def test_model_train_loss_parity(arch, sources):
     from tests._model_parity import check_step, oracle_bounds, run
     g, o, errs = run(sources=sources, arch=arch)
     assert g["loss"] == g["tail_loss"]
-    floor, sens = oracle_bounds(g, o, arch=arch)
-    check_step(g, o, errs, floor, sens, label=f"R{arch} {sources}")
+    b = oracle_bounds(g, o, arch=arch)
+    check_step(g, o, errs, b, label=f"R{arch} {sources}")
 
 
 @pytest.mark.parametrize("levels,target_id,source_ids", [((1, 3, 5), 1, (2, 3)), ((2, 4), 3, (1, 2)),
@@ -47,8 +48,8 @@ def test_model_general_levels_and_frame_ids(levels, target_id, source_ids):
     assert len(g["disps"]) == len(levels)
     for l, d in zip(levels, g["disps"]):
         assert d.shape[-2:] == (64 // 2 ** (5 - l), 128 // 2 ** (5 - l))
-    floor, sens = oracle_bounds(g, o, **kw)
-    check_step(g, o, errs, floor, sens, label=str(kw))
+    b = oracle_bounds(g, o, **kw)
+    check_step(g, o, errs, b, label=str(kw))
 
 
 def test_backward_segments_cover_params():

@@ -22,8 +22,8 @@ def test_mpi_train_step_parity(H, W, nb):
     assert g["loss"] == g["tail_loss"]
     # the plane axis is live: different bins, different disparities of the same sample
     assert (g["disps"][-1][0] - g["disps"][-1][1]).abs().max() > 0
-    floor, sens = oracle_bounds(g, o)
-    check_step(g, o, errs, floor, sens, label=f"MPI {W}x{H} planes {nb}")
+    b = oracle_bounds(g, o)
+    check_step(g, o, errs, b, label=f"MPI {W}x{H} planes {nb}")
 
 
 def test_mpi_mode_contract():

@@ -218,5 +218,5 @@ def test_model_automasking_parity():
     g, o, errs = run(sources="texture", automasking=True)
     assert g["loss"] == g["tail_loss"]
     assert (g["sel"] == -1).any(), "the automask never won: the test would not cover it"
-    floor, sens = oracle_bounds(g, o)
-    check_step(g, o, errs, floor, sens, label="automasking")
+    b = oracle_bounds(g, o)
+    check_step(g, o, errs, b, label="automasking")
