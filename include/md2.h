@@ -84,8 +84,10 @@ typedef struct md2_loss_out {
                                         (train_loss vis_warped, src/training.jl:71-73)        */
   int* vis_cell;                     /* [nscales][2][n][h][w] parity diagnostics: per pixel and
                                         source the grid_sample bilinear cell and border state,
-                                        x | y << 12 | sx << 24 | sy << 26 (0-based cell corner;
-                                        s = 0 interior, 1 clamped to 0, 2 clamped to W-1 / H-1) */
+                                        x | y << 11 | sx << 22 | sy << 24 (0-based cell corner;
+                                        s = 0 interior, 1 clamped to 0, 2 clamped to W-1 / H-1);
+                                        on the selected source, bits 26 + 2c = the L1 branch of
+                                        channel c (1 warped < target, 2 >, 3 equal); w, h <= 2048 */
 } md2_loss_out;
 
 /* disp[s]: [n][scale_h][scale_w]; pose: [2n][6] = (rvec, tvec) for (source s, sample i) at row

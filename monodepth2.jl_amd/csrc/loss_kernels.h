@@ -30,9 +30,13 @@ struct PhotoScale {
                           // diagnostics, PHOTO_CELL_* packing) or nullptr
 };
 
-// cell_map packing: x cell (bits 0-11), y cell (12-23), x border state (24-25), y (26-27);
-// state 0 = interior (coordinate differentiable), 1 = clamped to 0, 2 = clamped to W-1 / H-1
-constexpr int PHOTO_CELL_YSHIFT = 12, PHOTO_CELL_FXSHIFT = 24, PHOTO_CELL_FYSHIFT = 26;
+// cell_map packing: x cell (bits 0-10), y cell (11-21), x border state (22-23), y (24-25);
+// state 0 = interior (coordinate differentiable), 1 = clamped to 0, 2 = clamped to W-1 / H-1;
+// on the SELECTED source of a pixel, bits 26 + 2c: the L1 branch abs' took in channel c
+// (1 = warped below the target, 2 = above, 3 = equal: abs'(0) = 0; 0 on the other source)
+constexpr int PHOTO_CELL_YSHIFT = 11, PHOTO_CELL_FXSHIFT = 22, PHOTO_CELL_FYSHIFT = 24;
+constexpr int PHOTO_CELL_L1SHIFT = 26;
+constexpr int PHOTO_CELL_MAXDIM = 2048;
 
 struct PhotoArgs {
   PhotoScale sc[MAX_SCALES];

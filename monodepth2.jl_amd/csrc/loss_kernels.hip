@@ -333,23 +333,26 @@ __global__ __launch_bounds__(256) void pose_grad_reduce_kernel(FinalizeArgs a, f
 // so3_exp_map + composeT forward / backward (src/utils.jl:106-145, 185-192).
 // pose [2N][6] = (rvec, tvec) per (source, sample); invert flag per source.
 // ---------------------------------------------------------------------------------------------
+// fp64 throughout (2N threads): the rotation's rounding perturbs every pixel's warp coherently,
+// and 1 - cos(th) cancels at the small angles a pose network emits
 struct So3Tmp {
-  float S[9], S2[9], f1, f2, th, thi;
+  double S[9], S2[9], f1, f2, th, thi;
 };
 
-__device__ __forceinline__ void so3_core(const float* r, So3Tmp& t) {
-  t.S[0] = 0.f;   t.S[1] = -r[2]; t.S[2] = r[1];
-  t.S[3] = r[2];  t.S[4] = 0.f;   t.S[5] = -r[0];
-  t.S[6] = -r[1]; t.S[7] = r[0];  t.S[8] = 0.f;
+__device__ __forceinline__ void so3_core(const float* rf, So3Tmp& t) {
+  const double r[3] = {rf[0], rf[1], rf[2]};
+  t.S[0] = 0.0;   t.S[1] = -r[2]; t.S[2] = r[1];
+  t.S[3] = r[2];  t.S[4] = 0.0;   t.S[5] = -r[0];
+  t.S[6] = -r[1]; t.S[7] = r[0];  t.S[8] = 0.0;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       t.S2[3 * i + j] = t.S[3 * i] * t.S[j] + t.S[3 * i + 1] * t.S[3 + j] + t.S[3 * i + 2] * t.S[6 + j];
-  t.th = sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
-  t.thi = 1.f / fmaxf(t.th, 1e-4f);
-  t.f1 = t.thi * sinf(t.th);
-  t.f2 = t.thi * t.thi * (1.f - cosf(t.th));
+  t.th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+  t.thi = 1.0 / fmax(t.th, 1e-4);
+  t.f1 = t.thi * sin(t.th);
+  t.f2 = t.thi * t.thi * (1.0 - cos(t.th));
 }
 
 __global__ void so3_fwd_kernel(const float* __restrict__ pose, int count, int N, int invert_mask,
@@ -360,24 +363,24 @@ __global__ void so3_fwd_kernel(const float* __restrict__ pose, int count, int N,
   const float* r = pose + q * 6;
   So3Tmp t;
   so3_core(r, t);
-  float R[9];
+  double R[9];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) R[k] = t.f1 * t.S[k] + t.f2 * t.S2[k] + ((k % 4) == 0 ? 1.f : 0.f);
-  const float tv[3] = {pose[q * 6 + 3], pose[q * 6 + 4], pose[q * 6 + 5]};
+  for (int k = 0; k < 9; ++k) R[k] = t.f1 * t.S[k] + t.f2 * t.S2[k] + ((k % 4) == 0 ? 1.0 : 0.0);
+  const double tv[3] = {pose[q * 6 + 3], pose[q * 6 + 4], pose[q * 6 + 5]};
   float* o = Rt + q * 12;
   if ((invert_mask >> s) & 1) {
     // R' = R^T, t' = R' (-t)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) o[3 * i + j] = R[3 * j + i];
+      for (int j = 0; j < 3; ++j) o[3 * i + j] = (float)R[3 * j + i];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) o[9 + i] = -(o[3 * i] * tv[0] + o[3 * i + 1] * tv[1] + o[3 * i + 2] * tv[2]);
+    for (int i = 0; i < 3; ++i) o[9 + i] = (float)-(R[i] * tv[0] + R[3 + i] * tv[1] + R[6 + i] * tv[2]);
   } else {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) o[k] = R[k];
+    for (int k = 0; k < 9; ++k) o[k] = (float)R[k];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) o[9 + i] = tv[i];
+    for (int i = 0; i < 3; ++i) o[9 + i] = (float)tv[i];
   }
 }
 
@@ -390,15 +393,15 @@ __global__ void so3_bwd_kernel(const float* __restrict__ pose, int count, int N,
   const float* r = pose + q * 6;
   So3Tmp t;
   so3_core(r, t);
-  float R[9];
+  double R[9];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) R[k] = t.f1 * t.S[k] + t.f2 * t.S2[k] + ((k % 4) == 0 ? 1.f : 0.f);
-  const float tv[3] = {pose[q * 6 + 3], pose[q * 6 + 4], pose[q * 6 + 5]};
+  for (int k = 0; k < 9; ++k) R[k] = t.f1 * t.S[k] + t.f2 * t.S2[k] + ((k % 4) == 0 ? 1.0 : 0.0);
+  const double tv[3] = {pose[q * 6 + 3], pose[q * 6 + 4], pose[q * 6 + 5]};
   const float* g = dRt + q * 12;
-  float dR[9], dt[3];
+  double dR[9], dt[3];
   if ((invert_mask >> s) & 1) {
     // R' = R^T; t' = -R' t.  dR'_ij += -dt'_i t_j ;  dt = -R'^T dt' = -R dt'
-    float dRp[9];
+    double dRp[9];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -416,8 +419,8 @@ __global__ void so3_bwd_kernel(const float* __restrict__ pose, int count, int N,
     for (int i = 0; i < 3; ++i) dt[i] = g[9 + i];
   }
   // R = f1 S + f2 S^2 + I
-  float dS[9];
-  float df1 = 0.f, df2 = 0.f;
+  double dS[9];
+  double df1 = 0.0, df2 = 0.0;
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
     df1 += dR[k] * t.S[k];
@@ -428,7 +431,7 @@ __global__ void so3_bwd_kernel(const float* __restrict__ pose, int count, int N,
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      float a1 = 0.f, a2 = 0.f;
+      double a1 = 0.0, a2 = 0.0;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         a1 += dR[3 * i + k] * t.S[3 * j + k];
@@ -437,10 +440,10 @@ __global__ void so3_bwd_kernel(const float* __restrict__ pose, int count, int N,
       dS[3 * i + j] = t.f1 * dR[3 * i + j] + t.f2 * (a1 + a2);
     }
   // f1 = thi sin(th), f2 = thi^2 (1 - cos th), thi = 1/max(th, 1e-4)
-  const float dthi = (t.th > 1e-4f) ? -1.f / (t.th * t.th) : 0.f;
-  const float dth = df1 * (dthi * sinf(t.th) + t.thi * cosf(t.th)) +
-                    df2 * (2.f * t.thi * dthi * (1.f - cosf(t.th)) + t.thi * t.thi * sinf(t.th));
-  float dr[3];
+  const double dthi = (t.th > 1e-4) ? -1.0 / (t.th * t.th) : 0.0;
+  const double dth = df1 * (dthi * sin(t.th) + t.thi * cos(t.th)) +
+                     df2 * (2.0 * t.thi * dthi * (1.0 - cos(t.th)) + t.thi * t.thi * sin(t.th));
+  double dr[3];
   dr[0] = dS[7] - dS[5];            // hat rrule, src/utils.jl:139-141
   dr[1] = dS[2] - dS[6];
   dr[2] = dS[3] - dS[1];
@@ -450,14 +453,14 @@ __global__ void so3_bwd_kernel(const float* __restrict__ pose, int count, int N,
   if (accumulate) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      o[k] += dr[k];
-      o[3 + k] += dt[k];
+      o[k] = (float)(o[k] + dr[k]);
+      o[3 + k] = (float)(o[3 + k] + dt[k]);
     }
   } else {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      o[k] = dr[k];
-      o[3 + k] = dt[k];
+      o[k] = (float)dr[k];
+      o[3 + k] = (float)dt[k];
     }
   }
 }

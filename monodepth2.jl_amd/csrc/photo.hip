@@ -120,52 +120,57 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
   // and d u / d depth = (mt_0 (Kct_2 + 1e-7) - (Kct_0 - cx 1e-7) mt_2) / (camt_2 + 1e-7)^2 with the
   // depth terms cancelled exactly (mt = Mc (wc, hc, 1)).  For the usual K the maps are near
   // identity and every intermediate is a centred, small quantity.
+  // The maps are uniform per (sample, source): formed in fp64 and rounded once, since their
+  // rounding is a COHERENT perturbation of every pixel's warp (a tiny pose change), which the
+  // cancelling sums downstream (head-bias gradients) would see undiminished.
   const float cxp = g.K[2], cyp = g.K[5];
   float Kc[9];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    Kc[j] = g.K[j] - cxp * g.K[6 + j];
-    Kc[3 + j] = g.K[3 + j] - cyp * g.K[6 + j];
+    Kc[j] = fmaf(-cxp, g.K[6 + j], g.K[j]);
+    Kc[3 + j] = fmaf(-cyp, g.K[6 + j], g.K[3 + j]);
     Kc[6 + j] = g.K[6 + j];
-  }
-  float iKS[9];                                     // invK S
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    iKS[3 * i] = g.invK[3 * i];
-    iKS[3 * i + 1] = g.invK[3 * i + 1];
-    iKS[3 * i + 2] = fmaf(g.invK[3 * i], cxp, fmaf(g.invK[3 * i + 1], cyp, g.invK[3 * i + 2]));
-  }
-  float M[2][9], Kt[2][3];
-#pragma unroll
-  for (int sp = 0; sp < 2; ++sp) {
-    const float* rt = a.Rt + ((long)sp * a.N + n) * 12;
-    float KR[9];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        KR[3 * i + j] = Kc[3 * i] * rt[j] + Kc[3 * i + 1] * rt[3 + j] + Kc[3 * i + 2] * rt[6 + j];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        M[sp][3 * i + j] = KR[3 * i] * iKS[j] + KR[3 * i + 1] * iKS[3 + j] + KR[3 * i + 2] * iKS[6 + j];
-      Kt[sp][i] = Kc[3 * i] * rt[9] + Kc[3 * i + 1] * rt[10] + Kc[3 * i + 2] * rt[11];
-    }
   }
   // Mc rows + Kct, invK S rows and the depth-derivative constants in LDS, read where used (keeps
   // ~40 uniform floats out of VGPRs)
   __shared__ float4 s_cam[11];
   if (lane < 11) {
-    const int sp = lane / 3, i = lane % 3;
+    const double cxd = g.K[2], cyd = g.K[5];
+    double Kd[9], iKS[9];                           // Kc and invK S
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      Kd[j] = (double)g.K[j] - cxd * g.K[6 + j];
+      Kd[3 + j] = (double)g.K[3 + j] - cyd * g.K[6 + j];
+      Kd[6 + j] = g.K[6 + j];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      iKS[3 * i] = g.invK[3 * i];
+      iKS[3 * i + 1] = g.invK[3 * i + 1];
+      iKS[3 * i + 2] = (double)g.invK[3 * i] * cxd + (double)g.invK[3 * i + 1] * cyd + g.invK[3 * i + 2];
+    }
     float4 v;
-    if (lane < 6)
-      v = make_float4(M[sp][3 * i], M[sp][3 * i + 1], M[sp][3 * i + 2], Kt[sp][i]);
-    else if (lane < 9)
-      v = make_float4(iKS[3 * (lane - 6)], iKS[3 * (lane - 6) + 1], iKS[3 * (lane - 6) + 2], 0.f);
-    else {
+    if (lane < 6) {
+      const int sp = lane / 3, i = lane % 3;
+      const float* rt = a.Rt + ((long)sp * a.N + n) * 12;
+      double KR[3], m[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        KR[j] = Kd[3 * i] * rt[j] + Kd[3 * i + 1] * rt[3 + j] + Kd[3 * i + 2] * rt[6 + j];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) m[j] = KR[0] * iKS[j] + KR[1] * iKS[3 + j] + KR[2] * iKS[6 + j];
+      const double kt = Kd[3 * i] * rt[9] + Kd[3 * i + 1] * rt[10] + Kd[3 * i + 2] * rt[11];
+      v = make_float4((float)m[0], (float)m[1], (float)m[2], (float)kt);
+    } else if (lane < 9) {
+      const int r = lane - 6;
+      v = make_float4((float)iKS[3 * r], (float)iKS[3 * r + 1], (float)iKS[3 * r + 2], 0.f);
+    } else {
       const int q = lane - 9;
-      v = make_float4(Kt[q][0] - cxp * 1e-7f, Kt[q][1] - cyp * 1e-7f, Kt[q][2] + 1e-7f, 0.f);
+      const float* rt = a.Rt + ((long)q * a.N + n) * 12;
+      double kt[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) kt[i] = Kd[3 * i] * rt[9] + Kd[3 * i + 1] * rt[10] + Kd[3 * i + 2] * rt[11];
+      v = make_float4((float)(kt[0] - cxd * 1e-7), (float)(kt[1] - cyd * 1e-7), (float)(kt[2] + 1e-7), 0.f);
     }
     s_cam[lane] = v;
   }
@@ -328,14 +333,14 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
         for (int k = 0; k < 8; ++k) m[k] = m[k] + from_left(m[k]) + from_right(m[k]);
       }
       const float my = m[0] * inv9;                 // shifted mean of the target window
-      const float mty = my + cc[c];
+      const float mty = fmaf(m[0], inv9, cc[c]);
       const float vy = fmaf(m[1], inv9, -my * my);
       const float two_mty = 2.f * mty;
       const float B1y = fmaf(mty, mty, c1), B2y = vy + c2;
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp) {
         const float mx = m[2 + 3 * sp] * inv9;
-        const float mtx = mx + cc[c];
+        const float mtx = fmaf(m[2 + 3 * sp], inv9, cc[c]);
         const float vx = fmaf(m[3 + 3 * sp], inv9, -mx * mx);
         const float cxy = fmaf(m[4 + 3 * sp], inv9, -mx * my);
         const float A1 = fmaf(mtx, two_mty, c1), A2 = fmaf(2.f, cxy, c2);
@@ -385,6 +390,7 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
     const float* v1 = s_v1 + SA * NV * 64 + lane;
     const float kLq = kL * gpq;
     float gx[2] = {0.f, 0.f}, gy[2] = {0.f, 0.f};
+    unsigned l1bits = 0;                           // CELLS only: the L1 branches taken at q
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const float yq = yr[SA][c];
@@ -392,6 +398,7 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
       const float xs = (selq == 1) ? xr[SA][1][c] : xr[SA][0][c];
       const float df = xs - yq;
       const float t = df > 0.f ? kLq : (df < 0.f ? -kLq : 0.f);
+      if (CELLS) l1bits |= (df > 0.f ? 2u : (df < 0.f ? 1u : 3u)) << (PHOTO_CELL_L1SHIFT + 2 * c);
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp) {
         const int f = (sp * C + c) * 3;
@@ -409,6 +416,10 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
       }
     }
     const bool live = live3 && outl;
+    if (CELLS && live && selq >= 0) {              // parity diagnostics only (same lane wrote it)
+      int* cm = sc.cell_map + (((long)selq * a.N + n) * H + q) * W + col;
+      *cm = (int)((unsigned)*cm | l1bits);
+    }
     const float depth = v1[(4 * C) * 64];
     const float h = (float)(q + 1) - cyp;
     float X[3];
@@ -507,10 +518,10 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
       for (int k = 0; k < 3; ++k) {
 #pragma unroll
         for (int l = 0; l < 3; ++l)
-          out[1 + 12 * sp + 3 * k + l] = Kc[k] * acc[12 * sp + l] + Kc[3 + k] * acc[12 * sp + 3 + l] +
-                                         Kc[6 + k] * acc[12 * sp + 6 + l];
-        out[1 + 12 * sp + 9 + k] = Kc[k] * acc[12 * sp + 9] + Kc[3 + k] * acc[12 * sp + 10] +
-                                   Kc[6 + k] * acc[12 * sp + 11];
+          out[1 + 12 * sp + 3 * k + l] =
+              fmaf(Kc[k], acc[12 * sp + l], fmaf(Kc[3 + k], acc[12 * sp + 3 + l], Kc[6 + k] * acc[12 * sp + 6 + l]));
+        out[1 + 12 * sp + 9 + k] =
+            fmaf(Kc[k], acc[12 * sp + 9], fmaf(Kc[3 + k], acc[12 * sp + 10], Kc[6 + k] * acc[12 * sp + 11]));
       }
     }
   }
@@ -551,6 +562,10 @@ int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st)
         set_error("photometric: cell_map must be given for every scale or none");
         return MD2_EINVAL;
       }
+    if (g.W > PHOTO_CELL_MAXDIM || g.H > PHOTO_CELL_MAXDIM) {
+      set_error("photometric: cell_map packs 11-bit cells (w, h <= 2048)");
+      return MD2_EINVAL;
+    }
   }
   const dim3 grid((unsigned)blocks), block(64);
   if (C == 3 && !cells)

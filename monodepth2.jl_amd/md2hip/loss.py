@@ -84,14 +84,15 @@ def pack_poses(poses):
 
 def loss_tail(disparities, poses, x, auto_loss, cache: TrainCache, params: Params, *,
               grads=True, smooth_weights=None, divisor=None, smooth_normalize=True,
-              dloss=1.0, sigmoid_grad=False, visualize=False):
+              dloss=1.0, sigmoid_grad=False, visualize=False, keep_workspace=False):
     """The body of ``train_loss`` after the model call (src/training.jl:25-77) and its pullback.
 
     disparities: list of [N,1,h,w] float32 CUDA tensors (one per scale); poses: list of
     (rvec [N,3], tvec [N,3]) per source; x: [N,L,C,H,W]; auto_loss: [N,1,H,W] or None.
     Returns a dict: loss [1], terms [nscales,2], d_disp (list), d_pose [2N,6] and, with
     ``visualize``, vis_loss / vis_sel [nscales,N,H,W] (training.jl:71-74 vis_loss) and
-    vis_warped [2,N,C,H,W] (both sources warped by the last scale, training.jl:71-73)."""
+    vis_warped [2,N,C,H,W] (both sources warped by the last scale, training.jl:71-73).
+    ``keep_workspace`` (diagnostics): also return the raw workspace as "workspace"."""
     import torch
     N, L, C_, H, W = x.shape
     dev = x.device
@@ -109,6 +110,8 @@ def loss_tail(disparities, poses, x, auto_loss, cache: TrainCache, params: Param
            "terms": torch.empty(len(disparities), 2, dtype=torch.float32, device=dev),
            "d_disp": [torch.empty_like(d) for d in disparities] if grads else [None] * len(disparities),
            "d_pose": torch.empty(2 * N, 6, dtype=torch.float32, device=dev) if grads else None}
+    if keep_workspace:
+        res["workspace"] = ws
     if visualize:
         res["vis_loss"] = torch.empty(len(disparities), N, H, W, dtype=torch.float32, device=dev)
         res["vis_sel"] = torch.empty(len(disparities), N, H, W, dtype=torch.int8, device=dev)

@@ -186,7 +186,7 @@ def grid_sample_border(image: torch.Tensor, grid: torch.Tensor) -> torch.Tensor:
 def grid_sample_border_forced(image: torch.Tensor, grid: torch.Tensor, cell: torch.Tensor):
     """Test hook (like ``_forced_min``): ``grid_sample_border`` with the bilinear cell and the
     border-clamp state of every sample IMPOSED.  ``cell`` [N,H,W] int32 packs the 0-based cell
-    corner x | y << 12 and the border states sx << 24 | sy << 26 (0 = interior: the coordinate
+    corner x | y << 11 and the border states sx << 22 | sy << 24 (0 = interior: the coordinate
     itself, differentiable; 1 = clamped to 0; 2 = clamped to W-1 / H-1: constant) -- the GPU's
     own decisions (md2_loss_out.vis_cell).  Where the decisions agree with the unforced sampler
     the value and gradient are NNlib's (align_corners unnormalise ((g+1)/2)(W-1), border clamp
@@ -199,8 +199,8 @@ def grid_sample_border_forced(image: torch.Tensor, grid: torch.Tensor, cell: tor
     ix = (grid[..., 0] + 1.0) * 0.5 * (W - 1)
     iy = (grid[..., 1] + 1.0) * 0.5 * (H - 1)
     cell = cell.long()
-    xi, yi = cell & 0xFFF, (cell >> 12) & 0xFFF
-    sx, sy = (cell >> 24) & 3, (cell >> 26) & 3
+    xi, yi = cell & 0x7FF, (cell >> 11) & 0x7FF
+    sx, sy = (cell >> 22) & 3, (cell >> 24) & 3
     xc = torch.where(sx == 0, ix, torch.where(sx == 1, torch.zeros((), dtype=dt),
                                               torch.full((), W - 1.0, dtype=dt)))
     yc = torch.where(sy == 0, iy, torch.where(sy == 1, torch.zeros((), dtype=dt),
@@ -247,9 +247,17 @@ def _first_argmin(losses: Sequence[torch.Tensor]) -> torch.Tensor:
     return out
 
 
-def photometric_loss(predicted: torch.Tensor, target: torch.Tensor, alpha: float = 0.85):
-    """``photometric_loss`` -- src/training.jl:1-7.  -> [N,1,H,W]."""
-    l1 = torch.mean(torch.abs(target - predicted), dim=1, keepdim=True)
+def photometric_loss(predicted: torch.Tensor, target: torch.Tensor, alpha: float = 0.85,
+                     l1_sign=None):
+    """``photometric_loss`` -- src/training.jl:1-7.  -> [N,1,H,W].  ``l1_sign`` (test hook, like
+    ``_forced_min``): (recorded, sign) from forced_l1_sign; where recorded, |target - predicted|
+    is taken as sign * (predicted - target) -- the GPU's own abs' branch, which matters where the
+    difference is at fp32 rounding size (a recorded tie contributes 0, not the fp64 residue)."""
+    d = torch.abs(target - predicted)
+    if l1_sign is not None:
+        rec, sgn = l1_sign
+        d = torch.where(rec, sgn * (predicted - target), d)
+    l1 = torch.mean(d, dim=1, keepdim=True)
     s = torch.mean(ssim(predicted, target), dim=1, keepdim=True)
     return alpha * s + (1.0 - alpha) * l1
 
@@ -309,6 +317,16 @@ def poses_to_transforms(poses, source_ids, target_id):
     return [composeT(rvec, tvec, sid < target_id) for (rvec, tvec), sid in zip(poses, source_ids)]
 
 
+def forced_l1_sign(cell: torch.Tensor, C: int):
+    """The L1 branches the GPU recorded in vis_cell (bits 26 + 2c per channel c, on each pixel's
+    selected source only: 1 warped below the target, 2 above, 3 equal -- abs'(0) = 0):
+    [N,H,W] int32 -> (recorded [N,C,H,W] bool, sign [N,C,H,W] in {-1, 0, +1})."""
+    cell = cell.long() & 0xFFFFFFFF
+    code = torch.stack([(cell >> (26 + 2 * c)) & 3 for c in range(C)], 1)
+    sign = torch.where(code == 2, 1, torch.where(code == 1, -1, 0)).to(torch.int8)
+    return code != 0, sign
+
+
 def _forced_min(cands: Sequence[torch.Tensor], sel: torch.Tensor) -> torch.Tensor:
     """Test hook: the min over candidates with the argmin imposed (sel[p] = chosen index, where
     index 0 is the automask when present).  Same value as _first_argmin wherever the choice is
@@ -325,7 +343,8 @@ def loss_from_outputs(disparities, poses, x, auto_loss, cache: TrainCache, param
     """The body of ``train_loss`` after the model call -- src/training.jl:25,29-77.
     disparities: list of [N,1,h,w] (one per scale); poses: list of (rvec [N,3], tvec [N,3]).
     Test hooks: ``forced_sel`` (per scale, the imposed argmin), ``forced_cells`` (per scale
-    [2,N,H,W], the imposed bilinear cells / border states of both sources)."""
+    [2,N,H,W], the imposed bilinear cells / border states of both sources and the L1 signs of
+    the selected one)."""
     width, height = params.target_size
     target_x = x[:, cache.target_id - 1]
     Ps = poses_to_transforms(poses, cache.source_ids, cache.target_id)
@@ -337,7 +356,12 @@ def loss_from_outputs(disparities, poses, x, auto_loss, cache: TrainCache, param
         warped = warp(disparity, x, Ps, cache.K, cache.invK, cache.source_ids,
                       params.min_depth, params.max_depth,
                       cells=None if forced_cells is None else forced_cells[len(parts)])
-        src_losses = [photometric_loss(p, target_x) for p in warped]
+        if forced_cells is None:
+            src_losses = [photometric_loss(p, target_x) for p in warped]
+        else:
+            fc = forced_cells[len(parts)]
+            src_losses = [photometric_loss(p, target_x, l1_sign=forced_l1_sign(fc[j], p.shape[1]))
+                          for j, p in enumerate(warped)]
         if per_source is not None:
             per_source.append([l.detach() for l in src_losses])
         if forced_sel is not None:

@@ -26,10 +26,10 @@ SCALES = (0.125, 0.25, 0.5, 1.0)
 
 def loss_tail_case(N=2, C=3, H=32, W=64, seed=7):
     """Fused loss tail (src/training.jl:25-77) fwd + pullback on affine-ramp sources."""
-    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=True)
-    K, invK = D.intrinsics(W, H)
-    disps = D.disparities(N, H, W, seed=seed + 4)
-    poses = D.poses(N, seed=seed + 6)
+    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=True, grid32=False)
+    K, invK = D.intrinsics(W, H, grid32=False)
+    disps = D.disparities(N, H, W, seed=seed + 4, grid32=False)
+    poses = D.poses(N, seed=seed + 6, grid32=False)
     dv = [d.clone().requires_grad_(True) for d in disps]
     pv = [(r.clone().requires_grad_(True), t.clone().requires_grad_(True)) for r, t in poses]
     per_source = []
@@ -69,8 +69,8 @@ def so3_case():
 def model_digest(N=1, C=3, H=64, W=128, seed=7):
     """Full train_loss + gradient of the mono model (ResNet-18, scale_levels 2:5, Flux init seed
     42) at 64x128: loss, outputs and per-tensor gradient digests (norm, sum, 4 sampled entries)."""
-    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=True)
-    K, invK = D.intrinsics(W, H)
+    x = D.triplets(N, C, H, W, seed=seed, ramp_sources=True, grid32=False)
+    K, invK = D.intrinsics(W, H, grid32=False)
     spec = O.param_spec(18, C, (2, 3, 4, 5))
     flat = O.init_params(spec, 42).double().requires_grad_(True)
     P = O.unflatten(flat, spec)

@@ -16,7 +16,7 @@ def cells_of(grid, W, H):
     yi = torch.clamp(yc.floor().long(), max=H - 2)
     sx = torch.where(ix <= 0, 1, torch.where(ix >= W - 1, 2, 0))
     sy = torch.where(iy <= 0, 1, torch.where(iy >= H - 1, 2, 0))
-    return (xi | (yi << 12) | (sx << 24) | (sy << 26)).int()
+    return (xi | (yi << 11) | (sx << 22) | (sy << 24)).int()
 
 
 def test_forced_sampler_matches_grid_sample():
@@ -51,3 +51,26 @@ def test_forced_sampler_continues_the_imposed_cell():
     y.sum().backward()
     # d value / d pixel-x in cell [1, 2] is 5 - 1 = 4; d pixel-x / d grid-x = (W - 1) / 2 = 1
     assert abs(grid.grad[0, 0, 0, 0].item() - 4.0) < 1e-12
+
+
+def test_forced_l1_sign_decoding_and_branch():
+    """vis_cell's L1 branch codes (bits 26 + 2c: 1 warped below target, 2 above, 3 equal, 0 not
+    recorded) decode to (recorded, sign); a recorded branch opposite to the fp64 difference flips
+    abs' at that pixel only, a recorded tie gives abs'(0) = 0, with the value unchanged up to the
+    rounding-sized difference itself."""
+    code = (2 << 26) | (1 << 28) | (2 << 30)                     # channels: above, below, above
+    cell = torch.tensor([[[0, code - 2**32, (1 << 26) | (3 << 28) | (1 << 30)]]], dtype=torch.int32).expand(1, 2, 3)
+    rec, s = O.forced_l1_sign(cell, 3)
+    assert rec.shape == s.shape == (1, 3, 2, 3)
+    assert rec[0, :, 0, 0].tolist() == [False] * 3
+    assert rec[0, :, 0, 1].tolist() == [True] * 3 and s[0, :, 0, 1].tolist() == [1, -1, 1]
+    assert rec[0, :, 0, 2].tolist() == [True] * 3 and s[0, :, 0, 2].tolist() == [-1, 0, -1]
+    tgt = torch.zeros(1, 3, 2, 3, dtype=torch.float64)
+    pred = torch.full((1, 3, 2, 3), -1e-9, dtype=torch.float64).requires_grad_(True)
+    l = O.photometric_loss(pred, tgt, alpha=0.0, l1_sign=(rec, s))
+    l.sum().backward()
+    assert abs(l[0, 0, 0, 1].item()) < 1e-8
+    # pixel 0 unforced: abs' = sign(pred - tgt) = -1; pixel 1 forced [+, -, +]; pixel 2 [-, 0, -]
+    assert torch.allclose(pred.grad[0, :, 0, 0], torch.full((3,), -1 / 3, dtype=torch.float64))
+    assert torch.allclose(pred.grad[0, :, 0, 1], torch.tensor([1 / 3, -1 / 3, 1 / 3], dtype=torch.float64))
+    assert torch.allclose(pred.grad[0, :, 0, 2], torch.tensor([-1 / 3, 0.0, -1 / 3], dtype=torch.float64))

@@ -13,5 +13,5 @@ base=$(basename "$UNIT" .hip)
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 $FLAGS \
   -c "$C/$UNIT" -o "$OUT/$base.o"
 objs=$(ls "$C"/build/*.o | grep -v "/$base.o$")
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libmd2hip.so" $objs "$OUT/$base.o"
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libmd2hip.so" $objs "$OUT/$base.o" -lz
 echo "$OUT/libmd2hip.so"

@@ -36,18 +36,19 @@ print(f"loss gpu {g['loss'].item():.8f} f64 {l64:.8f} f32 {l32:.8f}")
 for s in range(len(SC)):
     print(f"scale {s}: d_disp gpu {D.rel_err(g['d_disp'][s], g64[s]):.2e}  fp32-oracle {D.rel_err(g32[s], g64[s]):.2e}")
 print(f"d_pose gpu {D.rel_err(g['d_pose'], p64):.2e}  fp32-oracle {D.rel_err(p32, p64):.2e}")
-s = len(SC) - 1
+s = int(os.environ.get("SCALE", len(SC) - 1))
 e = (g["d_disp"][s].double() - g64[s]).abs().flatten()
 e32 = (g32[s] - g64[s]).abs().flatten()
 rms = g64[s].pow(2).mean().sqrt().item()
-print(f"full res: rms |g| {rms:.3e}; gpu err quantiles (/rms)",
+print(f"scale {s}: rms |g| {rms:.3e}; gpu err quantiles (/rms)",
       [f"{q:.1e}" for q in (torch.quantile(e, torch.tensor([0.5, 0.9, 0.99, 0.999, 1.0], dtype=e.dtype)) / rms).tolist()])
 print("           fp32-oracle err quantiles (/rms)",
       [f"{q:.1e}" for q in (torch.quantile(e32, torch.tensor([0.5, 0.9, 0.99, 0.999, 1.0], dtype=e.dtype)) / rms).tolist()])
 top = torch.topk(e, 10).indices
 for i in top.tolist():
-    n, r = divmod(i, H * W)
-    yy, xx = divmod(r, W)
-    cs = cells[s, :, n, yy, xx]
+    hs, ws = g64[s].shape[-2:]
+    n, r = divmod(i, hs * ws)
+    yy, xx = divmod(r, ws)
+    cs = cells[s, :, n, yy, xx] if hs == H else cells[s, :, n, 0, 0]
     print(f"  n{n} ({yy},{xx}) g64 {g64[s].flatten()[i]:+.3e} gpu {g['d_disp'][s].flatten()[i].item():+.3e} "
-          f"f32 {g32[s].flatten()[i]:+.3e} sel {sel[s][n, 0, yy, xx].item()} states {[(c.item() >> 24) & 15 for c in cs]}")
+          f"f32 {g32[s].flatten()[i]:+.3e} sel {sel[s][n, 0, yy, xx].item() if hs == H else '-'} states {[(c.item() >> 22) & 15 for c in cs]}")
