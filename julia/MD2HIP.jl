@@ -42,12 +42,14 @@ struct ModelCfg                                        # md2_model_cfg
     embedding_levels::Cint; num_bins::Cint
 end
 
-# Params / TrainCache of src/Monodepth.jl:37-60 -> md2_model_cfg
-function ModelCfg(arch, in_ch, scale_levels, p, c)
+# Params / TrainCache of src/Monodepth.jl:37-60 -> md2_model_cfg.  MPI mode (src/model.jl:1-55):
+# embedding_levels = 21 (DepthDecoder(; embedding_levels)) and num_bins disparity planes, batch 1
+function ModelCfg(arch, in_ch, scale_levels, p, c; embedding_levels=0, num_bins=1)
     ModelCfg(arch, in_ch, p.batch_size, p.target_size..., length(scale_levels),
              pad5(scale_levels, Cint), rowmajor(c.K), rowmajor(c.invK),
              p.min_depth, p.max_depth, p.disparity_smoothness, pad5(c.scales, Cfloat),
-             p.automasking, c.target_id - 1, c.source_ids[1] - 1, c.source_ids[2] - 1)
+             p.automasking, c.target_id - 1, c.source_ids[1] - 1, c.source_ids[2] - 1,
+             embedding_levels, num_bins)
 end
 
 struct LossCfg                                         # md2_loss_cfg
@@ -607,6 +609,54 @@ function train_step_dp!(m::HIPModel, comm::Ptr{Cvoid}, x, auto_loss, η; β=(0.9
                  Cfloat, Cfloat, Cfloat, Cfloat, Cint, Ptr{Float32}, Ptr{Cvoid}),
                 m.handle, comm, x, ptr(auto_loss), m.m, m.v, η, β[1], β[2], ϵ, m.step, loss, stream_ptr()))
     return loss
+end
+
+# MPI mode: the disparity bins of the next train_loss, [batch][num_bins] on the device -- the
+# uniformly_sample_disparity_from_linspace_bins draw of src/model.jl:17-21 (CUDA.rand there)
+function set_disparity_bins!(m::HIPModel, bins::ROCArray{Float32,2})
+    check(ccall((:md2_model_set_disparity_bins, lib), Cint, (Ptr{Cvoid}, Ptr{Float32}, Ptr{Cvoid}),
+                m.handle, bins, stream_ptr()))
+    return m
+end
+
+# ------------------------------------------------------------------------------------------------
+# Data path (src/dtk.jl:29-46 Depth10k + FlipX, src/kitty.jl:45-61 KittyDataset): PNGs decoded on
+# the host's cores into N0f8 bytes, widened to Float32 on the GPU
+# ------------------------------------------------------------------------------------------------
+function png_size(path::AbstractString)
+    w, h, c = Ref{Cint}(0), Ref{Cint}(0), Ref{Cint}(0)
+    check(ccall((:md2_png_info, lib), Cint, (Cstring, Ref{Cint}, Ref{Cint}, Ref{Cint}), path, w, h, c))
+    return (w[], h[], c[])
+end
+
+function _to_device(bytes::Vector{UInt8}, dims)
+    d8 = ROCArray(bytes)
+    out = ROCArray{Float32}(undef, dims...)
+    check(ccall((:md2_unorm8_to_float, lib), Cint, (Ptr{UInt8}, Ptr{Float32}, Clonglong, Ptr{Cvoid}),
+                d8, out, length(bytes), stream_ptr()))
+    return out
+end
+
+# Depth10k triplets (3W x H side-by-side RGB PNGs) -> x::(W, H, 3, 3, n) Float32 on the device
+function load_triplets(paths::Vector{String}, width, height; flip=falses(length(paths)), threads=Threads.nthreads())
+    n = length(paths)
+    buf = Vector{UInt8}(undef, n * 3 * 3 * height * width)
+    fl = UInt8.(flip)
+    check(ccall((:md2_load_triplets_u8, lib), Cint,
+                (Ptr{Cstring}, Cint, Cint, Cint, Ptr{UInt8}, Ptr{UInt8}, Cint),
+                paths, n, width, height, fl, buf, threads))
+    return _to_device(buf, (width, height, 3, 3, n))
+end
+
+# KittyDataset: paths[3i+k] = frame k of sample i (8-bit gray), imresize'd to (height, width)
+function load_kitti(paths::Vector{String}, height, width; flip=falses(length(paths) ÷ 3), threads=Threads.nthreads())
+    n = length(paths) ÷ 3
+    buf = Vector{UInt8}(undef, n * 3 * height * width)
+    fl = UInt8.(flip)
+    check(ccall((:md2_load_kitti_u8, lib), Cint,
+                (Ptr{Cstring}, Cint, Cint, Cint, Ptr{UInt8}, Ptr{UInt8}, Cint),
+                paths, n, height, width, fl, buf, threads))
+    return _to_device(buf, (width, height, 1, 3, n))
 end
 
 end # module
