@@ -8,6 +8,7 @@
 //   * parameters / gradients are caller-owned flat fp32 vectors in the order of
 //     oracle/md2_oracle.py param_spec; conv weights are re-packed K-major after each update.
 #include "model.h"
+#include "head.h"
 
 #include <algorithm>
 #include <cmath>
@@ -473,6 +474,11 @@ class Model {
     if (h != cfg.H || w != cfg.W) {
       // the final branch must come back to full resolution for the loss (levels up to 5)
     }
+    if (batched_heads) {
+      HeadJob jobs[MAX_HEADS];
+      const int nh = head_jobs(jobs, ND);
+      if (nh > 0) MD2_TRY(alloc(&hws, heads_bwd_workspace(jobs, nh) / sizeof(float) + 64));
+    }
     // ---- pose decoder (2N pairs)
     const int h4 = featH[4], w4 = featW[4];
     const long hw4 = (long)h4 * w4;
@@ -606,6 +612,8 @@ class Model {
     if (pass && s)
       snprintf(r.tag, sizeof(r.tag), "%s %dx%d/%d%s %d->%d %dx%d n%d", pass, s->KH, s->KW, s->stride,
                s->reflect ? "r" : "", s->Cin, s->Cout, s->H, s->W, s->N);
+    else if (pass)
+      snprintf(r.tag, sizeof(r.tag), "%s", pass);
     recs.push_back(r);
   }
   static double conv_flops(const ConvShape& s) {
@@ -827,11 +835,55 @@ class Model {
         }
       }
       MD2_TRY(conv_f(d.c2, nimg, in, d.o2, co * hw2, ACT_ELU, 0, st));
-      if (d.head >= 0) MD2_TRY(conv_f(d.hc, nimg, tin(d.o2, co, hw2), d.disp, hw2, ACT_SIGMOID, 0, st));
+      if (d.head >= 0 && !batched_heads)
+        MD2_TRY(conv_f(d.hc, nimg, tin(d.o2, co, hw2), d.disp, hw2, ACT_SIGMOID, 0, st));
       x = d.o2;
       C = co;
     }
+    if (batched_heads) {
+      HeadJob jobs[MAX_HEADS];
+      const int nh = head_jobs(jobs, nimg);
+      hipEvent_t e = prof_begin(st);
+      MD2_TRY(heads_fwd(jobs, nh, ACT_SIGMOID, st));
+      prof_end(e, PROF_CONV_OTHER, heads_flops(nimg), st, "heads fwd");
+    }
     return MD2_OK;
+  }
+
+  // the DepthDecoder's disparity heads as one batch (head.h): MD2_HEADS_BATCH=0 runs them one
+  // conv at a time (A/B)
+  const bool batched_heads = tuning_knob("MD2_HEADS_BATCH", 1) != 0;
+  float* hws = nullptr;
+  int head_jobs(HeadJob* jobs, int nimg) {
+    int n = 0;
+    for (auto& d : br) {
+      if (d.head < 0) continue;
+      HeadJob& j = jobs[n++];
+      j = HeadJob{};
+      const long hw2 = 4L * d.h * d.w;
+      j.x = conv_head_in(tin(d.o2, d.b.cout, hw2));
+      j.wf = conv_head_w(d.hc.s, 0, d.hc.wpf);
+      j.wd = conv_head_w(d.hc.s, 1, d.hc.wpd);
+      j.Cin = d.b.cout;
+      j.H = 2 * d.h;
+      j.W = 2 * d.w;
+      j.N = nimg;
+      j.bias = P(d.hc.p.b);
+      j.y = d.disp;
+      j.ybs = hw2;
+      j.dy = d.d_head;
+      j.dx = d.d_o2;
+      j.dxbs = (long)d.b.cout * hw2;
+      j.dw = grads + d.hc.p.w;
+      j.db = Gd(d.hc.p.b);
+    }
+    return n;
+  }
+  double heads_flops(int nimg) const {
+    double f = 0.0;
+    for (auto& d : br)
+      if (d.head >= 0) f += 2.0 * nimg * 4.0 * d.h * d.w * 9.0 * d.b.cout;
+    return f;
   }
 
   // PoseDecoder input of the 2N pairs: in place for the default ids, else the gathered pin
@@ -1100,11 +1152,20 @@ class Model {
     MD2_TRY(conv_wd(sq, B, tin(feat[4], featC[4], hw4), d_sq, d_f4, (long)featC[4] * hw4, 0, st));
     // ---- DepthDecoder backward (reverse branch order), over ND decoder images
     const int nb = (int)br.size();
+    if (batched_heads) {
+      // every head's data + filter gradient first (their d_head all come from the loss tail):
+      // d_o2 of a head branch is then the head's dx, and the next branch's c1 dgrad adds to it
+      HeadJob jobs[MAX_HEADS];
+      const int nh = head_jobs(jobs, ND);
+      hipEvent_t e = prof_begin(st);
+      MD2_TRY(heads_bwd(jobs, nh, hws, heads_bwd_workspace(jobs, nh) + 256, st));
+      prof_end(e, PROF_CONV_OTHER, 2.0 * heads_flops(ND), st, "heads bwd");
+    }
     for (int i = nb - 1; i >= 0; --i) {
       DecBranch& d = br[i];
       const long hw = (long)d.h * d.w, hw2 = 4 * hw;
       const int co = d.b.cout;
-      if (d.head >= 0) {
+      if (d.head >= 0 && !batched_heads) {
         MD2_TRY(conv_wd(d.hc, ND, tin(d.o2, co, hw2), d.d_head, d.d_o2, co * hw2, i < nb - 1 ? 1 : 0, st));
       }
       MD2_TRY(act_bias(d.o2, d.d_o2, DPRE, ND, co, hw2, ACT_ELU, st));
@@ -1151,7 +1212,7 @@ class Model {
         cin = br[i - 1].b.cout;
         xin = br[i - 1].o2;
         dx = br[i - 1].d_o2;
-        acc = 0;
+        acc = (batched_heads && br[i - 1].head >= 0) ? 1 : 0;   // on top of the head's dx
       }
       MD2_TRY(conv_wd(d.c1, ND, tin(xin, cin, hw), DO1, dx, (long)cin * hw, acc, st));
       if (i == 0 && E > 0)

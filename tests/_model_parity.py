@@ -193,7 +193,8 @@ def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_i
     Returns a dict:
       floor[k]      per-tensor error of the same oracle in fp32 vs fp64 (end to end), plus the
                     forward outputs' floors "__disp<s>", "__pose", "__loss";
-      floor_b[k]    fp32 vs fp64 of ``sub`` (the backward's own fp32 floor);
+      floor_b[k]    fp32 vs fp64 of ``sub`` (the backward's own fp32 floor), the larger of two
+                    fp32 realisations (as is, and with the constants jittered by +-1 ulp);
       coherent[k]   |sub(K, invK, poses each +-1 fp32 ulp) - sub| / |sub|: the sensitivity to a
                     coherent warp perturbation of the size of the GPU's fp32 warp constants
                     (the per-(sample, source) maps every pixel shares) -- large exactly for the
@@ -216,8 +217,14 @@ def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_i
     s64, _, _, _ = _oracle_grad(g, torch.float64, at_gpu=True, **kw)
     s32, _, _, _ = _oracle_grad(g, torch.float32, at_gpu=True, **kw)
     sj, _, _, _ = _oracle_grad(g, torch.float64, at_gpu=True, jitter=11, **kw)
-    return {"floor": floor, "floor_b": per_tensor(spec, s32, s64), "explained": per_tensor(spec, s64, g64),
-            "coherent": per_tensor(spec, sj, s64), "bwd": per_tensor(spec, g["grad"].double(), s64)}
+    # a second fp32 realisation (the constants +-1 ulp): one fp32 sample of a cancelling sum's
+    # error can sit far below its typical size; the floor is the larger of the two
+    s32j, _, _, _ = _oracle_grad(g, torch.float32, at_gpu=True, jitter=11, **kw)
+    fb = per_tensor(spec, s32, s64)
+    fbj = per_tensor(spec, s32j, sj)
+    return {"floor": floor, "floor_b": {k: max(fb[k], fbj[k]) for k in fb},
+            "explained": per_tensor(spec, s64, g64), "coherent": per_tensor(spec, sj, s64),
+            "bwd": per_tensor(spec, g["grad"].double(), s64)}
 
 
 def check_step(g, o, errs, b, label=""):
