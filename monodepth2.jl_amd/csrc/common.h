@@ -112,6 +112,11 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t off_by
 __device__ __forceinline__ float bload_s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
 }
+// two consecutive floats at a 4-byte-aligned offset (the two taps of a bilinear row pair)
+__device__ __forceinline__ float2 bload2_s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
+  return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+}
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, 0);
   return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),

@@ -21,6 +21,10 @@ static int check_u31(long n) {
   return MD2_OK;
 }
 
+// units in flight per thread and trip in the BN reduction passes (all loads issued before the
+// first is summed; the sums take the units in the one-unit-per-trip order: bit-identical)
+constexpr int BN_INFLIGHT = 4;
+
 // One block per (channel c, image group p): the group's images x HW elements of channel c,
 // walked as a flat range (float4 units when HW % 4 == 0); fp64 accumulation.
 // SLAB: y is not read but formed here from the split-K slabs of the conv that produced it
@@ -39,12 +43,12 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
   const uint32_t nu = (uint32_t)(i1 - i0) * U;
   const long sstride = (long)C * N * HW;           // one slab [C][N*HW]
   double s = 0.0, ss = 0.0;
-  // two units per thread and trip (both loads in flight first), summed in the one-unit order
-  for (uint32_t e0 = threadIdx.x; e0 < nu; e0 += 512) {
-    float4 vv[2];
-    bool live[2];
+  // BN_INFLIGHT units per thread and trip (all loads in flight first), summed in the one-unit order
+  for (uint32_t e0 = threadIdx.x; e0 < nu; e0 += 256u * BN_INFLIGHT) {
+    float4 vv[BN_INFLIGHT];
+    bool live[BN_INFLIGHT];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < BN_INFLIGHT; ++h) {
       const uint32_t e = e0 + 256u * h;
       live[h] = e < nu;
       vv[h] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -71,7 +75,7 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < BN_INFLIGHT; ++h) {
       if (!live[h]) continue;
       const float4 v = vv[h];
       if (VEC) {
@@ -264,14 +268,26 @@ __device__ __forceinline__ void bn_finalise_plane(const BNStatsIn& s, int c, dou
   }
 }
 
-template <bool VEC>
+// Units per thread of the fused apply passes: a block covers 256 * UPT consecutive units, so the
+// per-block finalise (one wave per plane) is paid once per 256 * UPT units and a thread has UPT
+// independent loads in flight.  UPT only regroups the same per-element arithmetic (bit-identical
+// for every UPT).  The host picks the largest UPT that keeps >= BN_MIN_BLOCKS blocks and the
+// block's plane count within the 256-entry LDS tables.
+constexpr int BN_MIN_BLOCKS = 1024;
+static int bn_upt(long units, long U) {
+  int upt = 8;
+  while (upt > 1 && (units / (256L * upt) < BN_MIN_BLOCKS || 256L * upt / U + 2 > 256)) upt /= 2;
+  return upt;
+}
+
+template <bool VEC, int UPT = 1>
 __global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNApplyFused p, float* __restrict__ out,
                                                              uint32_t nu, FastDiv fdU, FastDiv fdC,
                                                              double total) {
   __shared__ float s_sc[256], s_sh[256], s_sc2[256], s_sh2[256];
-  const uint32_t u0 = blockIdx.x * 256u;
+  const uint32_t u0 = blockIdx.x * (256u * UPT);
   const uint32_t pl0 = fdiv(u0, fdU);
-  const uint32_t npl = fdiv(min(u0 + 255u, nu - 1u), fdU) - pl0 + 1u;
+  const uint32_t npl = fdiv(min(u0 + 256u * UPT - 1u, nu - 1u), fdU) - pl0 + 1u;
   for (uint32_t t = threadIdx.x >> 6; t < npl; t += 4) {   // wave-uniform plane loop
     const uint32_t pl = pl0 + t;
     const int c = (int)(pl - fdiv(pl, fdC) * fdC.d);
@@ -288,39 +304,53 @@ __global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNApplyFused p, flo
     }
   }
   __syncthreads();
-  const uint32_t u = u0 + threadIdx.x;
-  if (u >= nu) return;
-  const uint32_t li = fdiv(u, fdU) - pl0;
-  const float sc = s_sc[li], sh = s_sh[li];
-  float sc2 = 0.f, sh2 = 0.f;
-  if (p.y2) {
-    sc2 = s_sc2[li];
-    sh2 = s_sh2[li];
-  }
   if (VEC) {
-    const long i = 4L * u;
-    float4 v = *reinterpret_cast<const float4*>(p.y + i);
-    float r[4] = {__fmaf_rn(v.x, sc, sh), __fmaf_rn(v.y, sc, sh), __fmaf_rn(v.z, sc, sh),
-                  __fmaf_rn(v.w, sc, sh)};
-    if (p.y2) {
-      const float4 q = *reinterpret_cast<const float4*>(p.y2 + i);
-      r[0] += q.x * sc2 + sh2; r[1] += q.y * sc2 + sh2; r[2] += q.z * sc2 + sh2; r[3] += q.w * sc2 + sh2;
-    }
-    if (p.res) {
-      const float4 q = *reinterpret_cast<const float4*>(p.res + i);
-      r[0] += q.x; r[1] += q.y; r[2] += q.z; r[3] += q.w;
-    }
-    if (p.relu) {
+    // every load of the thread's UPT units in flight before the first is used
+    float4 v[UPT], q2[UPT], qr[UPT];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) r[k] = fmaxf(r[k], 0.f);
+    for (int j = 0; j < UPT; ++j) {
+      const uint32_t u = u0 + threadIdx.x + 256u * j;
+      const long i = 4L * (u < nu ? u : 0u);
+      v[j] = *reinterpret_cast<const float4*>(p.y + i);
+      if (p.y2) q2[j] = *reinterpret_cast<const float4*>(p.y2 + i);
+      if (p.res) qr[j] = *reinterpret_cast<const float4*>(p.res + i);
     }
-    *reinterpret_cast<float4*>(out + i) = make_float4(r[0], r[1], r[2], r[3]);
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const uint32_t u = u0 + threadIdx.x + 256u * j;
+      if (u >= nu) break;
+      const uint32_t li = fdiv(u, fdU) - pl0;
+      const float sc = s_sc[li], sh = s_sh[li];
+      float r[4] = {__fmaf_rn(v[j].x, sc, sh), __fmaf_rn(v[j].y, sc, sh), __fmaf_rn(v[j].z, sc, sh),
+                    __fmaf_rn(v[j].w, sc, sh)};
+      if (p.y2) {
+        const float sc2 = s_sc2[li], sh2 = s_sh2[li];
+        const float4 q = q2[j];
+        r[0] += q.x * sc2 + sh2; r[1] += q.y * sc2 + sh2; r[2] += q.z * sc2 + sh2; r[3] += q.w * sc2 + sh2;
+      }
+      if (p.res) {
+        const float4 q = qr[j];
+        r[0] += q.x; r[1] += q.y; r[2] += q.z; r[3] += q.w;
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = fmaxf(r[k], 0.f);
+      }
+      *reinterpret_cast<float4*>(out + 4L * u) = make_float4(r[0], r[1], r[2], r[3]);
+    }
   } else {
-    float r = __fmaf_rn(p.y[u], sc, sh);
-    if (p.y2) r += p.y2[u] * sc2 + sh2;
-    if (p.res) r += p.res[u];
-    if (p.relu) r = fmaxf(r, 0.f);
-    out[u] = r;
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const uint32_t u = u0 + threadIdx.x + 256u * j;
+      if (u >= nu) break;
+      const uint32_t li = fdiv(u, fdU) - pl0;
+      const float sc = s_sc[li], sh = s_sh[li];
+      float r = __fmaf_rn(p.y[u], sc, sh);
+      if (p.y2) r += p.y2[u] * s_sc2[li] + s_sh2[li];
+      if (p.res) r += p.res[u];
+      if (p.relu) r = fmaxf(r, 0.f);
+      out[u] = r;
+    }
   }
 }
 
@@ -331,8 +361,21 @@ int bn_apply_fused(const BNApplyFused& p, float* out, int N, int C, long HW, hip
                 "bn_apply_fused: missing statistics partials");
   const double total = (double)((long)N * HW);
   if (HW % 4 == 0) {
-    hipLaunchKernelGGL(bn_apply_fused_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st, p,
-                       out, (uint32_t)(n / 4), fd(HW / 4), fd(C), total);
+    const long nu = n / 4;
+    const int upt = bn_upt(nu, HW / 4);
+    const dim3 grid(cdiv(nu, 256L * upt));
+    if (upt == 8)
+      hipLaunchKernelGGL((bn_apply_fused_kernel<true, 8>), grid, dim3(256), 0, st, p, out, (uint32_t)nu,
+                         fd(HW / 4), fd(C), total);
+    else if (upt == 4)
+      hipLaunchKernelGGL((bn_apply_fused_kernel<true, 4>), grid, dim3(256), 0, st, p, out, (uint32_t)nu,
+                         fd(HW / 4), fd(C), total);
+    else if (upt == 2)
+      hipLaunchKernelGGL((bn_apply_fused_kernel<true, 2>), grid, dim3(256), 0, st, p, out, (uint32_t)nu,
+                         fd(HW / 4), fd(C), total);
+    else
+      hipLaunchKernelGGL((bn_apply_fused_kernel<true, 1>), grid, dim3(256), 0, st, p, out, (uint32_t)nu,
+                         fd(HW / 4), fd(C), total);
   } else {
     hipLaunchKernelGGL(bn_apply_fused_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st, p, out,
                        (uint32_t)n, fd(HW), fd(C), total);
@@ -388,13 +431,13 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
   const YMask ym = ymask(mgamma, mbeta, c, mu, is);
   const long sstride = (long)C * N * HW;
   double sg = 0.0, sgx = 0.0;
-  // two units per thread and trip (both loads in flight before either is used); the sums take
+  // BN_INFLIGHT units per thread and trip (all loads in flight before any is used); the sums take
   // them in the same order as one unit per trip
-  for (uint32_t e0 = threadIdx.x; e0 < nu; e0 += 512) {
-    float4 gv[2], yv[2];
-    bool live[2];
+  for (uint32_t e0 = threadIdx.x; e0 < nu; e0 += 256u * BN_INFLIGHT) {
+    float4 gv[BN_INFLIGHT], yv[BN_INFLIGHT];
+    bool live[BN_INFLIGHT];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < BN_INFLIGHT; ++h) {
       const uint32_t e = e0 + 256u * h;
       live[h] = e < nu;
       gv[h] = yv[h] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -435,7 +478,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < BN_INFLIGHT; ++h) {
       if (!live[h]) continue;
       float4 g = gv[h];
       const float4 v = yv[h];
@@ -633,7 +676,7 @@ int bn_bwd_apply(const float* dout, const float* mask_out, const float* y, const
 // ---- fused finalise + backward apply: per block the channels of its planes sum the backward
 // partials in bn_bwd_final_kernel's order (bit-identical dgamma/dbeta), the owner block of each
 // channel (first unit of image 0's plane) stores dgamma[c]/dbeta[c].
-template <bool VEC, bool SKIP = false>
+template <bool VEC, bool SKIP = false, int UPT = 1>
 __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
     const float* __restrict__ dout, const float* __restrict__ mask, const float* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -642,10 +685,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
     float invL, float* __restrict__ dy, float* __restrict__ dres, int dres_acc,
     const float* __restrict__ mbeta, SkipSrc pd = SkipSrc{}) {
   static_assert(!SKIP || VEC, "SKIP: float4 units of a read dout");
+  static_assert(VEC || UPT == 1, "scalar units: one per thread");
   __shared__ float s_k0[256], s_db[256], s_dg[256], s_mu[256], s_is[256], s_msc[256], s_msh[256];
-  const uint32_t u0 = blockIdx.x * 256u;
+  const uint32_t u0 = blockIdx.x * (256u * UPT);
   const uint32_t pl0 = fdiv(u0, fdU);
-  const uint32_t npl = fdiv(min(u0 + 255u, nu - 1u), fdU) - pl0 + 1u;
+  const uint32_t npl = fdiv(min(u0 + 256u * UPT - 1u, nu - 1u), fdU) - pl0 + 1u;
   for (uint32_t t = threadIdx.x >> 6; t < npl; t += 4) {   // one wave per plane (see bn_finalise_plane)
     const uint32_t pl = pl0 + t;
     const int c = (int)(pl - fdiv(pl, fdC) * fdC.d);
@@ -675,43 +719,57 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(
     }
   }
   __syncthreads();
-  const uint32_t u = u0 + threadIdx.x;
-  if (u >= nu) return;
-  const uint32_t li = fdiv(u, fdU) - pl0;
-  const float k0 = s_k0[li], db = s_db[li], dg = s_dg[li], mu = s_mu[li], is = s_is[li];
-  const YMask ym{s_msc[li], s_msh[li], mbeta != nullptr};
   if (VEC) {
-    const long i = 4L * u;
-    float g[4];
-    {
-      float4 t = *reinterpret_cast<const float4*>(dout + i);
-      if (SKIP) t = add_skip4(pd, (uint32_t)i, t);
-      g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
-    }
-    if (mask) {
-      const float4 m = *reinterpret_cast<const float4*>(mask + i);
-      if (!(m.x > 0.f)) g[0] = 0.f;
-      if (!(m.y > 0.f)) g[1] = 0.f;
-      if (!(m.z > 0.f)) g[2] = 0.f;
-      if (!(m.w > 0.f)) g[3] = 0.f;
-    }
-    const float4 v = *reinterpret_cast<const float4*>(y + i);
-    const float yv[4] = {v.x, v.y, v.z, v.w};
+    // every load of the thread's UPT units in flight before the first is used
+    float4 t[UPT], mv[UPT], v[UPT], qd[UPT];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) g[k] = ymasked(g[k], yv[k], ym);
-    float r[4];
+    for (int j = 0; j < UPT; ++j) {
+      const uint32_t u = u0 + threadIdx.x + 256u * j;
+      const long i = 4L * (u < nu ? u : 0u);
+      t[j] = *reinterpret_cast<const float4*>(dout + i);
+      if (SKIP) t[j] = add_skip4(pd, (uint32_t)i, t[j]);
+      if (mask) mv[j] = *reinterpret_cast<const float4*>(mask + i);
+      v[j] = *reinterpret_cast<const float4*>(y + i);
+      if (dres && dres_acc) qd[j] = *reinterpret_cast<const float4*>(dres + i);
+    }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = k0 * (g[k] - db - (yv[k] - mu) * is * dg);
-    *reinterpret_cast<float4*>(dy + i) = make_float4(r[0], r[1], r[2], r[3]);
-    if (dres) {
-      float4 o = make_float4(g[0], g[1], g[2], g[3]);
-      if (dres_acc) {
-        const float4 q = *reinterpret_cast<const float4*>(dres + i);
-        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+    for (int j = 0; j < UPT; ++j) {
+      const uint32_t u = u0 + threadIdx.x + 256u * j;
+      if (u >= nu) break;
+      const long i = 4L * u;
+      const uint32_t li = fdiv(u, fdU) - pl0;
+      const float k0 = s_k0[li], db = s_db[li], dg = s_dg[li], mu = s_mu[li], is = s_is[li];
+      const YMask ym{s_msc[li], s_msh[li], mbeta != nullptr};
+      float g[4] = {t[j].x, t[j].y, t[j].z, t[j].w};
+      if (mask) {
+        const float4 m = mv[j];
+        if (!(m.x > 0.f)) g[0] = 0.f;
+        if (!(m.y > 0.f)) g[1] = 0.f;
+        if (!(m.z > 0.f)) g[2] = 0.f;
+        if (!(m.w > 0.f)) g[3] = 0.f;
       }
-      *reinterpret_cast<float4*>(dres + i) = o;
+      const float yv[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] = ymasked(g[k], yv[k], ym);
+      float r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = k0 * (g[k] - db - (yv[k] - mu) * is * dg);
+      *reinterpret_cast<float4*>(dy + i) = make_float4(r[0], r[1], r[2], r[3]);
+      if (dres) {
+        float4 o = make_float4(g[0], g[1], g[2], g[3]);
+        if (dres_acc) {
+          const float4 q = qd[j];
+          o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+        }
+        *reinterpret_cast<float4*>(dres + i) = o;
+      }
     }
   } else {
+    const uint32_t u = u0 + threadIdx.x;
+    if (u >= nu) return;
+    const uint32_t li = fdiv(u, fdU) - pl0;
+    const float k0 = s_k0[li], db = s_db[li], dg = s_dg[li], mu = s_mu[li], is = s_is[li];
+    const YMask ym{s_msc[li], s_msh[li], mbeta != nullptr};
     float g = dout[u];
     if (mask && !(mask[u] > 0.f)) g = 0.f;
     g = ymasked(g, y[u], ym);
@@ -736,16 +794,27 @@ int bn_bwd_apply_fused(const float* dout, const float* mask_out, const float* y,
   MD2_CHECK_ARG(!sk.skip || (HW % 4 == 0 && sk.lo >= 0 && sk.lo <= sk.hi && sk.hi <= n),
                 "bn_bwd: skip range / HW % 4");
   const float invL = 1.f / (float)((long)N * HW);
-  if (sk.skip)
-    hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<true, true>), dim3(cdiv(n / 4, 256)), dim3(256), 0,
-                       st, dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
-                       (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy, dres, dres_accumulate, mbeta,
-                       skip_src(sk));
-  else if (HW % 4 == 0)
-    hipLaunchKernelGGL(bn_bwd_apply_fused_kernel<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, st,
-                       dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
-                       (uint32_t)(n / 4), fd(HW / 4), fd(C), invL, dy, dres, dres_accumulate, mbeta);
-  else
+  if (HW % 4 == 0) {
+    const long nu = n / 4;
+    const int upt = bn_upt(nu, HW / 4);
+    const dim3 grid(cdiv(nu, 256L * upt));
+#define MD2_BWDA(SK, U)                                                                              \
+  hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<true, SK, U>), grid, dim3(256), 0, st, dout, mask_out, y, \
+                     mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta, (uint32_t)nu, fd(HW / 4), \
+                     fd(C), invL, dy, dres, dres_accumulate, mbeta, skip_src(sk))
+    if (sk.skip) {
+      if (upt == 8) MD2_BWDA(true, 8);
+      else if (upt == 4) MD2_BWDA(true, 4);
+      else if (upt == 2) MD2_BWDA(true, 2);
+      else MD2_BWDA(true, 1);
+    } else {
+      if (upt == 8) MD2_BWDA(false, 8);
+      else if (upt == 4) MD2_BWDA(false, 4);
+      else if (upt == 2) MD2_BWDA(false, 2);
+      else MD2_BWDA(false, 1);
+    }
+#undef MD2_BWDA
+  } else
     hipLaunchKernelGGL(bn_bwd_apply_fused_kernel<false>, dim3(cdiv(n, 256)), dim3(256), 0, st,
                        dout, mask_out, y, mean, invstd, gamma, ws.partials, ws.parts, dgamma, dbeta,
                        (uint32_t)n, fd(HW), fd(C), invL, dy, dres, dres_accumulate, mbeta);

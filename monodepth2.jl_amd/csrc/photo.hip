@@ -267,14 +267,17 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
         sc.cell_map[(((long)sp * a.N + n) * H + R) * W + col] =
             xi | (yi << PHOTO_CELL_YSHIFT) | (fx << PHOTO_CELL_FXSHIFT) | (fy << PHOTO_CELL_FYSHIFT);
       }
+      // xi <= W-2, yi <= H-2: the right / lower taps are always +1 / +W, so each row pair of
+      // taps is ONE 8-byte load (half the gather instructions of four dword loads)
       const uint32_t vo = (uint32_t)(yi * W + xi) * 4u;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const uint32_t so = so_s[sp] + (uint32_t)c * HW4;
-        gv[sp][c][0] = bload_s(rxs, vo, so);
-        gv[sp][c][1] = bload_s(rxs, vo, so + 4u);
-        gv[sp][c][2] = bload_s(rxs, vo, so + W4);
-        gv[sp][c][3] = bload_s(rxs, vo, so + W4 + 4u);
+        const float2 t = bload2_s(rxs, vo, so), b = bload2_s(rxs, vo, so + W4);
+        gv[sp][c][0] = t.x;
+        gv[sp][c][1] = t.y;
+        gv[sp][c][2] = b.x;
+        gv[sp][c][3] = b.y;
       }
     }
     const uint32_t to = (uint32_t)(Rr * W + colr) * 4u;
