@@ -205,8 +205,12 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
   // upsample_bilinear to full resolution, align_corners (training.jl:45); the full-resolution
   // scale takes the same path with zero weights (exact)
   const float usx = sc.rx * (float)colr;
-  const int ux0 = min((int)usx, dw - 1), ux1 = min(ux0 + 1, dw - 1);
+  const int ux0 = min((int)usx, dw - 1);
   const float ufx = usx - (float)ux0;
+  // the two column taps ux0, min(ux0 + 1, dw - 1) as ONE 8-byte load at min(ux0, dw - 2): at the
+  // last column (ux0 = dw - 1) both taps are the pair's right element (dw >= 2)
+  const int uxp = min(ux0, dw - 2);
+  const bool uedge = ux0 == dw - 1;
   const float kS = a.wloss * (0.85f / (float)C) * (1.f / 9.f);
   const float kL = a.wloss * (0.15f / (float)C);
   const float inv9 = 1.f / 9.f, c1 = 1e-4f, c2 = 9e-4f;
@@ -229,17 +233,20 @@ void photo_stream_kernel(PhotoArgs a, Geom g, PhotoTiling tl) {
     const float sy = sc.ry * (float)reflect_clamp(R, H);
     const int uy0 = min((int)sy, dh - 1), uy1 = min(uy0 + 1, dh - 1);
     fyA = sy - (float)uy0;
-    dA[0] = bload(rdsp, (uint32_t)(uy0 * dw + ux0) * 4u);
-    dA[1] = bload(rdsp, (uint32_t)(uy0 * dw + ux1) * 4u);
-    dA[2] = bload(rdsp, (uint32_t)(uy1 * dw + ux0) * 4u);
-    dA[3] = bload(rdsp, (uint32_t)(uy1 * dw + ux1) * 4u);
+    const float2 t = bload2_s(rdsp, (uint32_t)(uy0 * dw + uxp) * 4u, 0u);
+    const float2 b = bload2_s(rdsp, (uint32_t)(uy1 * dw + uxp) * 4u, 0u);
+    dA[0] = t.x;
+    dA[1] = t.y;
+    dA[2] = b.x;
+    dA[3] = b.y;
   };
 
   auto issue_gathers = [&](int R) {
     const int Rr = reflect_clamp(R, H);
     const float h = (float)(Rr + 1) - cyp;
-    const float dtop = fmaf(ufx, dA[1] - dA[0], dA[0]);
-    const float dbot = fmaf(ufx, dA[3] - dA[2], dA[2]);
+    const float d00 = uedge ? dA[1] : dA[0], d10 = uedge ? dA[3] : dA[2];
+    const float dtop = fmaf(ufx, dA[1] - d00, d00);
+    const float dbot = fmaf(ufx, dA[3] - d10, d10);
     const float d = fmaf(fyA, dbot - dtop, dtop);
     const float depth = frcp(fmaf(d, g.disp_range, g.min_disp));   // disparity_to_depth
     bdepth = depth;
@@ -555,6 +562,11 @@ int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st)
     set_error("photometric: image must be at least 3x3");
     return MD2_EINVAL;
   }
+  for (int s = 0; s < a.nscales; ++s)
+    if (a.sc[s].dw < 2) {   // the disparity column taps are one 8-byte pair load
+      set_error("photometric: disparity maps must be at least 2 columns wide");
+      return MD2_EINVAL;
+    }
   const PhotoTiling tl = photo_tiling(g.W, g.H, a.N, a.nscales);
   const long blocks = tl.per_scale() * a.N * a.nscales;
   bool cells = false;
