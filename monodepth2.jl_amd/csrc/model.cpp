@@ -265,6 +265,53 @@ class Model {
   float *DA = nullptr, *DY = nullptr, *G = nullptr, *DYD = nullptr;
   float *DPRE = nullptr, *DUP = nullptr, *DO1 = nullptr;
   ConvWorkspace cws{};
+  // Side stream for two independent branches, each with its OWN scratch (split-K workspace,
+  // bias-gradient partials, activation-pullback buffer, BN partials slot 1) so they can run
+  // beside the model stream:
+  //  * the PoseDecoder depends only on the encoder's layer-4 features (forward) and on d_pose
+  //    from the loss tail (backward): it runs beside the DepthDecoder and joins before the loss
+  //    tail (poses) and before the decoder's first-branch dgrad accumulates into the layer-4
+  //    feature gradient the squeezer's dgrad wrote (MD2_POSE_STREAM);
+  //  * a downsampling block's 1x1 conv + BN depends only on the block input: its forward runs
+  //    beside the block's 3x3 chain and joins before the residual BN apply; its backward runs
+  //    beside the chain's backward and joins before the first conv's dgrad accumulates into the
+  //    block's input gradient the 1x1 dgrad wrote (MD2_DOWN_STREAM).
+  // The arithmetic is unchanged (same kernels, same buffers' contents): the step is
+  // bit-identical with either switch off (=0, tests/test_gpu_fusion.py) and under the HIP-event
+  // probe, which runs everything on the model stream so that its brackets time kernels alone.
+  ConvWorkspace cws_side{};
+  float* bp_ws_side = nullptr;
+  float* DPRE_side = nullptr;
+  bool side_ws = false;       // conv / act_bias calls of a side branch: its own scratch
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  const bool pose_stream = [] {
+    const char* v = getenv("MD2_POSE_STREAM");
+    return !(v && v[0] == '0');
+  }();
+  ConvWorkspace& ws_conv() { return side_ws ? cws_side : cws; }
+  float* ws_bp() { return side_ws ? bp_ws_side : bp_ws; }
+  const bool down_stream = [] {
+    const char* v = getenv("MD2_DOWN_STREAM");
+    return !(v && v[0] == '0');
+  }();
+  bool pose_overlap() const { return pose_stream && side && !prof; }
+  bool down_overlap() const { return down_stream && side && !prof; }
+  // the downsample branch's conv + BN statistics (slot 1), on `st`
+  int down_fwd(EncBlock& b, int nimg, hipStream_t st) {
+    side_ws = true;
+    const long ohw = (long)b.H * b.W;
+    const int rc = conv_f_bn(b.dconv, nimg, tin(b.in, b.Cin, (long)b.Hin * b.Win), b.yd, (long)b.C * ohw,
+                             b.dbn, ohw, st, 1);
+    side_ws = false;
+    return rc;
+  }
+  // ops of `st2` wait for everything enqueued on `st1` so far
+  int stream_wait(hipStream_t st1, hipStream_t st2, hipEvent_t e) {
+    MD2_HIP(hipEventRecord(e, st1));
+    MD2_HIP(hipStreamWaitEvent(st2, e, 0));
+    return MD2_OK;
+  }
   BNStatsWs bnws{};
   long bn_slot = 0;       // doubles per partials slot (slot 1: the downsample BN of a block)
   void* tail_ws = nullptr;
@@ -275,6 +322,9 @@ class Model {
 
   ~Model() {
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (side) (void)hipStreamDestroy(side);
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (join_ev) (void)hipEventDestroy(join_ev);
     if (g.st) (void)hipStreamDestroy(g.st);
     for (void* p : allocs) (void)hipFree(p);
     for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
@@ -354,7 +404,7 @@ class Model {
     NP = E > 0 ? cfg.num_bins : 1;
     ND = N * NP;
     const int C = A.in_ch;
-    size_t wsn = 0, scratch = 0;
+    size_t wsn = 0, wsn_side = 0, scratch = 0;   // wsn_side: the side-stream convs (downsample, pose)
     long bnmax = 0;
     auto track = [&](long n) { scratch = std::max(scratch, (size_t)n); };
     auto bnws_need = [&](int Cc, long HW) {
@@ -411,8 +461,8 @@ class Model {
         }
         if (bs.down) {
           eb.down = true;
-          MD2_TRY(make_conv(eb.dconv, bs.dconv, cH, cW, true, wsn));
-          need_ws(eb.dconv, B, wsn, true);
+          MD2_TRY(make_conv(eb.dconv, bs.dconv, cH, cW, true, wsn_side));
+          need_ws(eb.dconv, B, wsn_side, true);
           MD2_TRY(make_bn(eb.dbn, bs.dbn));
           MD2_TRY(alloc(&eb.yd, (long)B * bs.cout * h * w));
         }
@@ -482,12 +532,12 @@ class Model {
     // ---- pose decoder (2N pairs)
     const int h4 = featH[4], w4 = featW[4];
     const long hw4 = (long)h4 * w4;
-    MD2_TRY(make_conv(sq, spec.squeezer, h4, w4, true, wsn));
-    need_ws(sq, B, wsn, true);
-    MD2_TRY(make_conv(p1, spec.p1, h4, w4, true, wsn));
-    need_ws(p1, 2 * N, wsn, true);
-    MD2_TRY(make_conv(p2, spec.p2, h4, w4, true, wsn));
-    need_ws(p2, 2 * N, wsn, true);
+    MD2_TRY(make_conv(sq, spec.squeezer, h4, w4, true, wsn_side));
+    need_ws(sq, B, wsn_side, true);
+    MD2_TRY(make_conv(p1, spec.p1, h4, w4, true, wsn_side));
+    need_ws(p1, 2 * N, wsn_side, true);
+    MD2_TRY(make_conv(p2, spec.p2, h4, w4, true, wsn_side));
+    need_ws(p2, 2 * N, wsn_side, true);
     p1.cat = p2.cat = PROF_CONV3_ENC;     // zero-padded 3x3 like the encoder's (same kernels)
     MD2_TRY(alloc(&sqo, (long)B * 256 * hw4));
     MD2_TRY(alloc(&d_sq, (long)B * 256 * hw4));
@@ -522,6 +572,17 @@ class Model {
       cws.bytes = wsn + 256;
     }
     MD2_TRY(alloc(&bp_ws, BP_WS));
+    {
+      float* q;
+      MD2_TRY(alloc(&q, wsn_side / sizeof(float) + 64));
+      cws_side.ptr = q;
+      cws_side.bytes = wsn_side + 256;
+    }
+    MD2_TRY(alloc(&bp_ws_side, BP_WS));
+    MD2_TRY(alloc(&DPRE_side, 2L * N * 256 * hw4));
+    MD2_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    MD2_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+    MD2_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
     {
       double* q;
       void* v;
@@ -631,7 +692,7 @@ class Model {
     o.act = act;
     o.accumulate = accumulate;
     hipEvent_t e = prof_begin(st);
-    MD2_TRY(conv_fwd(s, in, c.wpf, o, cws, st));
+    MD2_TRY(conv_fwd(s, in, c.wpf, o, ws_conv(), st));
     prof_end(e, c.cat, conv_flops(s), st, "fwd", &s);
     return MD2_OK;
   }
@@ -648,7 +709,7 @@ class Model {
     o.bias = P(c.p.b);
     SplitKDefer d;
     hipEvent_t e = prof_begin(st);
-    MD2_TRY(conv_fwd(s, in, c.wpf, o, cws, st, fuse_splitk ? &d : nullptr));
+    MD2_TRY(conv_fwd(s, in, c.wpf, o, ws_conv(), st, fuse_splitk ? &d : nullptr));
     if (d.splits > 0) {
       BNStatsWs w = bn_ws(bn, nimg, HW, slot);
       MD2_TRY(bn_stats_partial_slabs(SlabIn{d.slab, d.splits}, y, nimg, bn.p.c, HW, w, st));
@@ -769,6 +830,12 @@ class Model {
         const float* x = b.in;
         int C = b.Cin;
         long HW = (long)b.Hin * b.Win;
+        const bool dov = b.down && down_overlap();
+        if (dov) {
+          MD2_TRY(stream_wait(st, side, fork_ev));
+          MD2_TRY(down_fwd(b, nimg, side));
+          MD2_HIP(hipEventRecord(join_ev, side));
+        }
         for (size_t k = 0; k < b.st.size(); ++k) {
           EncStage& e = b.st[k];
           const long ohw = (long)e.conv.s.Ho * e.conv.s.Wo;
@@ -787,7 +854,10 @@ class Model {
         BNApplyFused a{};
         a.y = last.y; a.s1 = bn_in(last.bn); a.relu = 1;
         if (b.down) {
-          MD2_TRY(conv_f_bn(b.dconv, nimg, tin(b.in, b.Cin, (long)b.Hin * b.Win), b.yd, (long)b.C * ohw, b.dbn, ohw, st, 1));
+          if (dov)
+            MD2_HIP(hipStreamWaitEvent(st, join_ev, 0));
+          else
+            MD2_TRY(down_fwd(b, nimg, st));
           a.y2 = b.yd; a.s2 = bn_in(b.dbn);
         } else {
           a.res = b.in;
@@ -896,6 +966,12 @@ class Model {
   }
 
   int pose_fwd(hipStream_t st) {
+    side_ws = true;
+    const int rc = pose_fwd_body(st);
+    side_ws = false;
+    return rc;
+  }
+  int pose_fwd_body(hipStream_t st) {
     const long hw4 = (long)featH[4] * featW[4];
     MD2_TRY(conv_f(sq, B, tin(feat[4], featC[4], hw4), sqo, 256 * hw4, ACT_RELU, 0, st));
     if (!pairs_inplace) MD2_TRY(pair_gather(sqo, N, 256, hw4, pa, pb, pin, st));
@@ -914,8 +990,15 @@ class Model {
     in.bs0 = 3 * fs;
     in.bhi = fs;
     MD2_TRY(encoder_fwd(in, B, st));
-    MD2_TRY(decoder_fwd(N, T0, st));
-    MD2_TRY(pose_fwd(st));
+    if (pose_overlap()) {
+      MD2_TRY(stream_wait(st, side, fork_ev));
+      MD2_TRY(pose_fwd(side));
+      MD2_TRY(decoder_fwd(N, T0, st));
+      MD2_TRY(stream_wait(side, st, join_ev));
+    } else {
+      MD2_TRY(decoder_fwd(N, T0, st));
+      MD2_TRY(pose_fwd(st));
+    }
     const float* disps[MAX_SCALES] = {};
     LossTailOut o{};
     int li = 0;
@@ -1007,7 +1090,7 @@ class Model {
     ConvShape s = c.s;
     s.N = nimg;
     hipEvent_t e = prof_begin(st);
-    MD2_TRY(conv_wgrad(s, in, dy, grads + c.p.w, Gd(c.p.b), 0, cws, st, c.p.b >= 0 ? bp_pending : nullptr,
+    MD2_TRY(conv_wgrad(s, in, dy, grads + c.p.w, Gd(c.p.b), 0, ws_conv(), st, c.p.b >= 0 ? bp_pending : nullptr,
                        bp_parts));
     bp_pending = nullptr;
     prof_end(e, c.cat, conv_flops(s), st, "wgrad", &s);
@@ -1033,7 +1116,7 @@ class Model {
     o.c0 = c0;
     o.accumulate = acc;
     hipEvent_t e = prof_begin(st);
-    MD2_TRY(conv_dgrad(s, dy, c.wpd, o, cws, st));
+    MD2_TRY(conv_dgrad(s, dy, c.wpd, o, ws_conv(), st));
     prof_end(e, c.cat, conv_flops(s), st, "dgrad", &s);
     return MD2_OK;
   }
@@ -1049,7 +1132,7 @@ class Model {
     o.bs0 = da_bs;
     SplitKDefer d;
     hipEvent_t e = prof_begin(st);
-    MD2_TRY(conv_dgrad(s, dy, c.wpd, o, cws, st, fuse_splitk ? &d : nullptr));
+    MD2_TRY(conv_dgrad(s, dy, c.wpd, o, ws_conv(), st, fuse_splitk ? &d : nullptr));
     if (d.splits == 0) {
       prof_end(e, c.cat, conv_flops(s), st, "dgrad", &s);
       return bn_bwd(bn, da, nullptr, y, nimg, HW, dyprev, nullptr, 0, st, true);
@@ -1073,8 +1156,8 @@ class Model {
       bp_pending = nullptr;
       return act_backward(out, dout, dpre, (long)nimg * C * HW, act, st);
     }
-    MD2_TRY(act_backward_bias(out, dout, dpre, nimg, C, HW, act, bp_ws, st));
-    bp_pending = bp_ws;
+    MD2_TRY(act_backward_bias(out, dout, dpre, nimg, C, HW, act, ws_bp(), st));
+    bp_pending = ws_bp();
     bp_parts = act_bias_parts(C, nimg, HW);
     return MD2_OK;
   }
@@ -1084,8 +1167,9 @@ class Model {
   // BN+ReLU (stem, intra-block): the mask is re-derived from y (bit-exact, one read less)
   int bn_bwd(RBN& bn, const float* dout, const float* mask, const float* y, int nimg, long HW,
              float* dy, float* dres, int dres_acc, hipStream_t st, bool relu_from_y = false,
-             SkipAdd sk = SkipAdd{}) {
+             SkipAdd sk = SkipAdd{}, int slot = 0) {
     BNStatsWs w = bnws;
+    w.partials += slot * bn_slot;
     w.parts = bn_parts(bn.p.c, nimg, HW);
     const float* mg = relu_from_y ? P(bn.p.g) : nullptr;
     const float* mb = relu_from_y ? P(bn.p.b) : nullptr;
@@ -1117,9 +1201,18 @@ class Model {
     EncStage& last = b.st.back();
     // last BN (+ residual, ReLU): g = (d_out [+ skip]) * relu'(out)
     MD2_TRY(bn_bwd(last.bn, b.d_out, last.a, last.y, nimg, ohw, DY, b.down ? G : b.d_in, 0, st, false, sk));
+    const bool dov = b.down && down_overlap();
     if (b.down) {
-      MD2_TRY(bn_bwd(b.dbn, G, nullptr, b.yd, nimg, ohw, DYD, nullptr, 0, st));
-      MD2_TRY(conv_wd(b.dconv, nimg, tin(b.in, b.Cin, ihw), DYD, b.d_in, (long)b.Cin * ihw, 0, st));
+      // downsample branch: BN backward (partials slot 1) + the 1x1 conv's filter and data
+      // gradients (d_in written whole; the chain's first conv adds to it below)
+      hipStream_t sd = dov ? side : st;
+      if (dov) MD2_TRY(stream_wait(st, side, fork_ev));
+      MD2_TRY(bn_bwd(b.dbn, G, nullptr, b.yd, nimg, ohw, DYD, nullptr, 0, sd, false, SkipAdd{}, 1));
+      side_ws = true;
+      const int rc = conv_wd(b.dconv, nimg, tin(b.in, b.Cin, ihw), DYD, b.d_in, (long)b.Cin * ihw, 0, sd);
+      side_ws = false;
+      MD2_TRY(rc);
+      if (dov) MD2_HIP(hipEventRecord(join_ev, side));
     }
     for (int k = ns - 1; k >= 0; --k) {
       EncStage& e = b.st[k];
@@ -1131,25 +1224,47 @@ class Model {
         EncStage& pe = b.st[k - 1];
         MD2_TRY(conv_d_bn(e.conv, nimg, DY, DA, (long)cin * hin, pe.bn, pe.y, hin, DY, st));
       } else {
+        if (dov) MD2_HIP(hipStreamWaitEvent(st, join_ev, 0));   // b.d_in written by the 1x1 dgrad
         MD2_TRY(conv_wd(e.conv, nimg, tin(xin, cin, hin), DY, b.d_in, (long)cin * hin, 1, st));
       }
     }
     return MD2_OK;
   }
 
-  int seg_decoder(hipStream_t st) {
+  // PoseDecoder backward: d_pose -> pose parameter gradients and the layer-4 feature gradient
+  // d_f4 (written whole by the squeezer's dgrad; the DepthDecoder's first branch adds to it)
+  int pose_bwd(hipStream_t st) {
+    side_ws = true;
+    const int rc = pose_bwd_body(st);
+    side_ws = false;
+    return rc;
+  }
+  int pose_bwd_body(hipStream_t st) {
     const long hw4 = (long)featH[4] * featW[4];
-    // ---- PoseDecoder backward
-    MD2_TRY(pose_head_bwd(d_pose, 2 * N, 256, hw4, P(spec.p3.w), means, DPRE, Gd(spec.p3.w),
+    float* DP = DPRE_side;
+    MD2_TRY(pose_head_bwd(d_pose, 2 * N, 256, hw4, P(spec.p3.w), means, DP, Gd(spec.p3.w),
                           Gd(spec.p3.b), st));
-    MD2_TRY(act_bias(pc2, DPRE, DPRE, 2 * N, 256, hw4, ACT_RELU, st));
-    MD2_TRY(conv_wd(p2, 2 * N, tin(pc1, 256, hw4), DPRE, d_pc1, 256 * hw4, 0, st));
+    MD2_TRY(act_bias(pc2, DP, DP, 2 * N, 256, hw4, ACT_RELU, st));
+    MD2_TRY(conv_wd(p2, 2 * N, tin(pc1, 256, hw4), DP, d_pc1, 256 * hw4, 0, st));
     MD2_TRY(act_bias(pc1, d_pc1, d_pc1, 2 * N, 256, hw4, ACT_RELU, st));
     MD2_TRY(conv_wd(p1, 2 * N, pose_pairs_in(hw4), d_pc1, d_pin, 512 * hw4, 0, st));
     MD2_TRY(pair_grad_gather(d_pin, N, 256, hw4, pa, pb, d_sq, st));
     MD2_TRY(act_bias(sqo, d_sq, d_sq, B, 256, hw4, ACT_RELU, st));
     float* d_f4 = stages[3].back().d_out;
-    MD2_TRY(conv_wd(sq, B, tin(feat[4], featC[4], hw4), d_sq, d_f4, (long)featC[4] * hw4, 0, st));
+    return conv_wd(sq, B, tin(feat[4], featC[4], hw4), d_sq, d_f4, (long)featC[4] * hw4, 0, st);
+  }
+
+  int seg_decoder(hipStream_t st) {
+    // ---- PoseDecoder backward: beside the DepthDecoder's on the side stream, or first
+    const bool ov = pose_overlap();
+    if (ov) {
+      MD2_TRY(stream_wait(st, side, fork_ev));
+      MD2_TRY(pose_bwd(side));
+      MD2_HIP(hipEventRecord(join_ev, side));
+    } else {
+      MD2_TRY(pose_bwd(st));
+    }
+    float* d_f4 = stages[3].back().d_out;
     // ---- DepthDecoder backward (reverse branch order), over ND decoder images
     const int nb = (int)br.size();
     if (batched_heads) {
@@ -1198,6 +1313,7 @@ class Model {
       int cin;
       float* dx;
       int acc;
+      if (i == 0 && ov) MD2_HIP(hipStreamWaitEvent(st, join_ev, 0));   // d_f4 written by the squeezer
       if (i == 0 && E > 0) {
         cin = featC[4] + E;
         xin = emb_in[4];
