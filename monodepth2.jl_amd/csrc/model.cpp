@@ -295,7 +295,18 @@ class Model {
     const char* v = getenv("MD2_DOWN_STREAM");
     return !(v && v[0] == '0');
   }();
+  const bool dec_wgrad_stream = [] {
+    const char* v = getenv("MD2_DEC_WGRAD_STREAM");
+    return !(v && v[0] == '0');
+  }();
+  // DepthDecoder backward: each conv's filter gradient on the side stream beside its data
+  // gradient and the rest of the branch (the decoder convs fill a fraction of the chip).  The
+  // side reads DPRE / DO1 and the bias partials of the act_bias before it, so those buffers are
+  // reused only after the side's event (bias partials double-buffered: bp_dec[0] for c2, [1] for c1)
+  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c2 = nullptr, ev_c1 = nullptr;
+  float* bp_dec[2] = {nullptr, nullptr};
   bool pose_overlap() const { return pose_stream && side && !prof; }
+  bool wgrad_overlap() const { return dec_wgrad_stream && side && !prof; }
   bool down_overlap() const { return down_stream && side && !prof; }
   // the downsample branch's conv + BN statistics (slot 1), on `st`
   int down_fwd(EncBlock& b, int nimg, hipStream_t st) {
@@ -324,6 +335,8 @@ class Model {
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (side) (void)hipStreamDestroy(side);
     if (fork_ev) (void)hipEventDestroy(fork_ev);
+    for (hipEvent_t e : {ev_a, ev_b, ev_c2, ev_c1})
+      if (e) (void)hipEventDestroy(e);
     if (join_ev) (void)hipEventDestroy(join_ev);
     if (g.st) (void)hipStreamDestroy(g.st);
     for (void* p : allocs) (void)hipFree(p);
@@ -404,7 +417,7 @@ class Model {
     NP = E > 0 ? cfg.num_bins : 1;
     ND = N * NP;
     const int C = A.in_ch;
-    size_t wsn = 0, wsn_side = 0, scratch = 0;   // wsn_side: the side-stream convs (downsample, pose)
+    size_t wsn = 0, wsn_side = 0, scratch = 0;   // wsn_side: side-stream convs (downsample, pose, decoder wgrad)
     long bnmax = 0;
     auto track = [&](long n) { scratch = std::max(scratch, (size_t)n); };
     auto bnws_need = [&](int Cc, long HW) {
@@ -493,6 +506,8 @@ class Model {
       need_ws(d.c1, ND, wsn, true);
       MD2_TRY(make_conv(d.c2, bs.c2, 2 * h, 2 * w, true, wsn));
       need_ws(d.c2, ND, wsn, true);
+      need_ws(d.c1, ND, wsn_side, false);   // filter gradients on the side stream (wgrad_overlap)
+      need_ws(d.c2, ND, wsn_side, false);
       MD2_TRY(alloc(&d.o1, (long)ND * bs.cout * h * w));
       MD2_TRY(alloc(&d.up, (long)ND * bs.cout * 4 * h * w));
       MD2_TRY(alloc(&d.o2, (long)ND * bs.cout * 4 * h * w));
@@ -583,6 +598,9 @@ class Model {
     MD2_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     MD2_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     MD2_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
+    for (hipEvent_t* e : {&ev_a, &ev_b, &ev_c2, &ev_c1}) MD2_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    MD2_TRY(alloc(&bp_dec[0], BP_WS));
+    MD2_TRY(alloc(&bp_dec[1], BP_WS));
     {
       double* q;
       void* v;
@@ -1151,13 +1169,14 @@ class Model {
   const float* bp_pending = nullptr;
   int bp_parts = 0;
   int act_bias(const float* out, const float* dout, float* dpre, int nimg, int C, long HW, int act,
-               hipStream_t st) {
+               hipStream_t st, float* bp_buf = nullptr) {
     if (HW % 4 != 0 || (long)C * act_bias_parts(C, nimg, HW) > BP_WS) {
       bp_pending = nullptr;
       return act_backward(out, dout, dpre, (long)nimg * C * HW, act, st);
     }
-    MD2_TRY(act_backward_bias(out, dout, dpre, nimg, C, HW, act, ws_bp(), st));
-    bp_pending = ws_bp();
+    float* bp = bp_buf ? bp_buf : ws_bp();
+    MD2_TRY(act_backward_bias(out, dout, dpre, nimg, C, HW, act, bp, st));
+    bp_pending = bp;
     bp_parts = act_bias_parts(C, nimg, HW);
     return MD2_OK;
   }
@@ -1276,6 +1295,18 @@ class Model {
       MD2_TRY(heads_bwd(jobs, nh, hws, heads_bwd_workspace(jobs, nh) + 256, st));
       prof_end(e, PROF_CONV_OTHER, 2.0 * heads_flops(ND), st, "heads bwd");
     }
+    const bool wov = wgrad_overlap();
+    // filter gradient of conv c on the side stream once the main stream has reached `ready`
+    auto wgrad_side = [&](RConv& c, const TensorIn& in, const float* dy, hipEvent_t ready,
+                          hipEvent_t done) -> int {
+      MD2_TRY(stream_wait(st, side, ready));
+      side_ws = true;
+      const int rc = conv_w(c, ND, in, dy, side);
+      side_ws = false;
+      MD2_TRY(rc);
+      MD2_HIP(hipEventRecord(done, side));
+      return MD2_OK;
+    };
     for (int i = nb - 1; i >= 0; --i) {
       DecBranch& d = br[i];
       const long hw = (long)d.h * d.w, hw2 = 4 * hw;
@@ -1283,7 +1314,8 @@ class Model {
       if (d.head >= 0 && !batched_heads) {
         MD2_TRY(conv_wd(d.hc, ND, tin(d.o2, co, hw2), d.d_head, d.d_o2, co * hw2, i < nb - 1 ? 1 : 0, st));
       }
-      MD2_TRY(act_bias(d.o2, d.d_o2, DPRE, ND, co, hw2, ACT_ELU, st));
+      if (wov && i < nb - 1) MD2_HIP(hipStreamWaitEvent(st, ev_c2, 0));   // DPRE, bp_dec[0] free
+      MD2_TRY(act_bias(d.o2, d.d_o2, DPRE, ND, co, hw2, ACT_ELU, st, wov ? bp_dec[0] : nullptr));
       TensorIn in = tin(d.up, co, hw2);
       float* dskip = nullptr;
       long skip_bs = 0;
@@ -1301,14 +1333,20 @@ class Model {
           skip_bs = (long)featC[fi] * hw2;
         }
       }
-      MD2_TRY(conv_wd(d.c2, ND, in, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
+      if (wov) {
+        MD2_TRY(wgrad_side(d.c2, in, DPRE, ev_a, ev_c2));
+        MD2_TRY(conv_d(d.c2, ND, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
+      } else {
+        MD2_TRY(conv_wd(d.c2, ND, in, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
+      }
       if (E > 0 && d.b.cskip > 0) {
         // _repeat pullback: the skip gradient of the target features = sum over the planes
         const int fi = 4 - d.b.bid;
         MD2_TRY(plane_sum(d_emb[fi], N, NP, featC[fi] + E, featC[fi], hw2, d_skip[fi], 0, st));
       }
+      if (wov && i < nb - 1) MD2_HIP(hipStreamWaitEvent(st, ev_c1, 0));   // DO1, bp_dec[1] free
       MD2_TRY(upsample2_bwd(DUP, ND, co, d.h, d.w, DO1, st));
-      MD2_TRY(act_bias(d.o1, DO1, DO1, ND, co, hw, ACT_ELU, st));
+      MD2_TRY(act_bias(d.o1, DO1, DO1, ND, co, hw, ACT_ELU, st, wov ? bp_dec[1] : nullptr));
       const float* xin;
       int cin;
       float* dx;
@@ -1330,10 +1368,16 @@ class Model {
         dx = br[i - 1].d_o2;
         acc = (batched_heads && br[i - 1].head >= 0) ? 1 : 0;   // on top of the head's dx
       }
-      MD2_TRY(conv_wd(d.c1, ND, tin(xin, cin, hw), DO1, dx, (long)cin * hw, acc, st));
+      if (wov) {
+        MD2_TRY(wgrad_side(d.c1, tin(xin, cin, hw), DO1, ev_b, ev_c1));
+        MD2_TRY(conv_d(d.c1, ND, DO1, dx, (long)cin * hw, acc, st));
+      } else {
+        MD2_TRY(conv_wd(d.c1, ND, tin(xin, cin, hw), DO1, dx, (long)cin * hw, acc, st));
+      }
       if (i == 0 && E > 0)
         MD2_TRY(plane_sum(d_emb[4], N, NP, cin, featC[4], hw, d_f4 + (long)T0 * featC[4] * hw, 1, st));
     }
+    if (wov) MD2_HIP(hipStreamWaitEvent(st, ev_c1, 0));   // every decoder filter gradient final
     return MD2_OK;
   }
 
