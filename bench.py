@@ -330,7 +330,7 @@ def main():
                                            "achieved": round(gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                            "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": ptraffic,
                                            "traffic_source": psrc,
-                                           "note": "VALU-issue bound, not HBM-bound: profiles/r02_pmc_photo.json",
+                                           "note": "issue-bound (waves 64% active at 2 waves/SIMD, 1141 VALU instr per pixel-scale), not HBM-bound: profiles/r03_pmc_photo.json, DESIGN.md sec. 4",
                                            "launches": n, "algorithmic_bytes_per_step": byt,
                                            "kernel_ms_per_step": round(ms, 4)}
             ms2, flop2, n2 = prof["conv_other"]
