@@ -265,7 +265,7 @@ class Model {
   float *DA = nullptr, *DY = nullptr, *G = nullptr, *DYD = nullptr;
   float *DPRE = nullptr, *DUP = nullptr, *DO1 = nullptr;
   ConvWorkspace cws{};
-  // Side stream for two independent branches, each with its OWN scratch (split-K workspace,
+  // Side stream for independent branches, each with its OWN scratch (split-K workspace,
   // bias-gradient partials, activation-pullback buffer, BN partials slot 1) so they can run
   // beside the model stream:
   //  * the PoseDecoder depends only on the encoder's layer-4 features (forward) and on d_pose
@@ -275,9 +275,10 @@ class Model {
   //  * a downsampling block's 1x1 conv + BN depends only on the block input: its forward runs
   //    beside the block's 3x3 chain and joins before the residual BN apply; its backward runs
   //    beside the chain's backward and joins before the first conv's dgrad accumulates into the
-  //    block's input gradient the 1x1 dgrad wrote (MD2_DOWN_STREAM).
+  //    block's input gradient the 1x1 dgrad wrote (MD2_DOWN_STREAM);
+  //  * the DepthDecoder's filter gradients beside its data gradients (MD2_DEC_WGRAD_STREAM, below).
   // The arithmetic is unchanged (same kernels, same buffers' contents): the step is
-  // bit-identical with either switch off (=0, tests/test_gpu_fusion.py) and under the HIP-event
+  // bit-identical with any switch off (=0, tests/test_gpu_fusion.py) and under the HIP-event
   // probe, which runs everything on the model stream so that its brackets time kernels alone.
   ConvWorkspace cws_side{};
   float* bp_ws_side = nullptr;
