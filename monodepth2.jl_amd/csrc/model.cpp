@@ -309,6 +309,29 @@ class Model {
   bool pose_overlap() const { return pose_stream && side && !prof; }
   bool wgrad_overlap() const { return dec_wgrad_stream && side && !prof; }
   bool down_overlap() const { return down_stream && side && !prof; }
+  // Encoder backward of the last stage (stages >= enc_wgrad_from: layer 4 by default; its convs
+  // are small and split-K): each block conv's filter gradient on the side stream beside its data
+  // gradient (interleaved A/B, 3 x 60 steps: off 1481, from layer 4 1493, from layer 3 1490,
+  // from layer 2 1478 images/s -- the larger layers' convs fill the chip and only time-share).  The
+  // conv's dY alternates between DY and DY2 so the data gradient's BN backward can write the next
+  // dY while the side still reads the current one; a dY buffer is written again only after the
+  // side's event for its last read (ev_y[j]); every stage segment ends with the side joined.
+  const bool enc_wgrad_stream = [] {
+    const char* v = getenv("MD2_ENC_WGRAD_STREAM");
+    return !(v && v[0] == '0');
+  }();
+  const int enc_wgrad_from = tuning_knob("MD2_ENC_WGRAD_FROM", 3);
+  bool enc_overlap(int si) const { return enc_wgrad_stream && side && !prof && si >= enc_wgrad_from; }
+  float* DY2 = nullptr;
+  hipEvent_t ev_y[2] = {nullptr, nullptr};
+  bool y_pending[2] = {false, false};
+  int ycur = 0;
+  float* ybuf(int j) { return j ? DY2 : DY; }
+  int y_claim(int j, hipStream_t st) {   // the model stream is about to write dY buffer j
+    if (y_pending[j]) MD2_HIP(hipStreamWaitEvent(st, ev_y[j], 0));
+    y_pending[j] = false;
+    return MD2_OK;
+  }
   // the downsample branch's conv + BN statistics (slot 1), on `st`
   int down_fwd(EncBlock& b, int nimg, hipStream_t st) {
     side_ws = true;
@@ -336,7 +359,7 @@ class Model {
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (side) (void)hipStreamDestroy(side);
     if (fork_ev) (void)hipEventDestroy(fork_ev);
-    for (hipEvent_t e : {ev_a, ev_b, ev_c2, ev_c1})
+    for (hipEvent_t e : {ev_a, ev_b, ev_c2, ev_c1, ev_y[0], ev_y[1]})
       if (e) (void)hipEventDestroy(e);
     if (join_ev) (void)hipEventDestroy(join_ev);
     if (g.st) (void)hipStreamDestroy(g.st);
@@ -463,6 +486,7 @@ class Model {
           MD2_TRY(make_conv(es.conv, bs.convs[k], h, w, true, wsn));
           es.conv.cat = bs.convs[k].k == 3 ? PROF_CONV3_ENC : PROF_CONV_OTHER;
           need_ws(es.conv, B, wsn, true);
+          need_ws(es.conv, B, wsn_side, false);   // filter gradient on the side (enc_overlap)
           MD2_TRY(make_bn(es.bn, bs.bns[k]));
           h = es.conv.s.Ho;
           w = es.conv.s.Wo;
@@ -576,6 +600,7 @@ class Model {
     // ---- scratch / workspaces
     MD2_TRY(alloc(&DA, scratch));
     MD2_TRY(alloc(&DY, scratch));
+    MD2_TRY(alloc(&DY2, scratch));
     MD2_TRY(alloc(&G, scratch));
     MD2_TRY(alloc(&DYD, scratch));
     MD2_TRY(alloc(&DPRE, scratch));
@@ -599,7 +624,8 @@ class Model {
     MD2_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     MD2_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     MD2_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
-    for (hipEvent_t* e : {&ev_a, &ev_b, &ev_c2, &ev_c1}) MD2_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    for (hipEvent_t* e : {&ev_a, &ev_b, &ev_c2, &ev_c1, &ev_y[0], &ev_y[1]})
+      MD2_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     MD2_TRY(alloc(&bp_dec[0], BP_WS));
     MD2_TRY(alloc(&bp_dec[1], BP_WS));
     {
@@ -1214,13 +1240,15 @@ class Model {
     return sk;
   }
 
-  int block_bwd(EncBlock& b, hipStream_t st, SkipAdd sk = SkipAdd{}) {
+  int block_bwd(EncBlock& b, hipStream_t st, SkipAdd sk = SkipAdd{}, bool eov = false) {
     const int nimg = B;
     const long ohw = (long)b.H * b.W, ihw = (long)b.Hin * b.Win;
     const int ns = (int)b.st.size();
     EncStage& last = b.st.back();
     // last BN (+ residual, ReLU): g = (d_out [+ skip]) * relu'(out)
-    MD2_TRY(bn_bwd(last.bn, b.d_out, last.a, last.y, nimg, ohw, DY, b.down ? G : b.d_in, 0, st, false, sk));
+    MD2_TRY(y_claim(ycur, st));
+    MD2_TRY(bn_bwd(last.bn, b.d_out, last.a, last.y, nimg, ohw, ybuf(ycur), b.down ? G : b.d_in, 0, st,
+                   false, sk));
     const bool dov = b.down && down_overlap();
     if (b.down) {
       // downsample branch: BN backward (partials slot 1) + the 1x1 conv's filter and data
@@ -1239,13 +1267,27 @@ class Model {
       const float* xin = k == 0 ? b.in : b.st[k - 1].a;
       const int cin = e.conv.p.cin;
       const long hin = (long)e.conv.s.H * e.conv.s.W;
+      float* dy = ybuf(ycur);
+      if (eov) {   // filter gradient beside the data gradient; dy untouched until ev_y[ycur]
+        MD2_TRY(stream_wait(st, side, fork_ev));
+        side_ws = true;
+        const int rc = conv_w(e.conv, nimg, tin(xin, cin, hin), dy, side);
+        side_ws = false;
+        MD2_TRY(rc);
+        MD2_HIP(hipEventRecord(ev_y[ycur], side));
+        y_pending[ycur] = true;
+      } else {
+        MD2_TRY(conv_w(e.conv, nimg, tin(xin, cin, hin), dy, st));
+      }
       if (k > 0) {
-        MD2_TRY(conv_w(e.conv, nimg, tin(xin, cin, hin), DY, st));
         EncStage& pe = b.st[k - 1];
-        MD2_TRY(conv_d_bn(e.conv, nimg, DY, DA, (long)cin * hin, pe.bn, pe.y, hin, DY, st));
+        const int nx = ycur ^ 1;
+        MD2_TRY(y_claim(nx, st));
+        MD2_TRY(conv_d_bn(e.conv, nimg, dy, DA, (long)cin * hin, pe.bn, pe.y, hin, ybuf(nx), st));
+        ycur = nx;
       } else {
         if (dov) MD2_HIP(hipStreamWaitEvent(st, join_ev, 0));   // b.d_in written by the 1x1 dgrad
-        MD2_TRY(conv_wd(e.conv, nimg, tin(xin, cin, hin), DY, b.d_in, (long)cin * hin, 1, st));
+        MD2_TRY(conv_d(e.conv, nimg, dy, b.d_in, (long)cin * hin, 1, st));
       }
     }
     return MD2_OK;
@@ -1385,7 +1427,8 @@ class Model {
   int seg_stage(int si, hipStream_t st) {
     auto& sg = stages[si];
     for (int k = (int)sg.size() - 1; k >= 0; --k)
-      MD2_TRY(block_bwd(sg[k], st, k == (int)sg.size() - 1 ? skip_add(si + 1) : SkipAdd{}));
+      MD2_TRY(block_bwd(sg[k], st, k == (int)sg.size() - 1 ? skip_add(si + 1) : SkipAdd{}, enc_overlap(si)));
+    for (int j = 0; j < 2; ++j) MD2_TRY(y_claim(j, st));   // the stage's filter gradients final
     if (si >= 1 && !skip_fused(si)) {
       // d f_si (= block 0's d_in) += decoder skip gradient on the target slice
       const long n = (long)N * featC[si] * featH[si] * featW[si];

@@ -7,8 +7,9 @@ BN + ReLU + max pool in one forward kernel (MD2_FUSE_POOL_FWD), the stem's decod
 added by the max-pool adjoint (MD2_FUSE_POOL_BWD), and the encoder stages' skip gradients added
 inside the BN-backward passes instead of by axpy (MD2_FUSE_SKIP_BWD).  And the PoseDecoder on its own
 stream beside the DepthDecoder, and the downsampling blocks' 1x1 conv + BN beside the block's 3x3
-chain, and the DepthDecoder's filter gradients beside its data gradients, each with its own scratch
-(MD2_POSE_STREAM, MD2_DOWN_STREAM, MD2_DEC_WGRAD_STREAM)."""
+chain, and the DepthDecoder's and the late encoder stages' filter gradients beside their data
+gradients, each with its own scratch (MD2_POSE_STREAM, MD2_DOWN_STREAM, MD2_DEC_WGRAD_STREAM,
+MD2_ENC_WGRAD_STREAM)."""
 import os
 
 import pytest
@@ -42,7 +43,7 @@ def _setup(fuse, H, W, B, switch="MD2_FUSE_SPLITK"):
 
 @pytest.mark.parametrize("switch", ["MD2_FUSE_SPLITK", "MD2_FUSE_POOL_FWD", "MD2_FUSE_POOL_BWD",
                                     "MD2_FUSE_SKIP_BWD", "MD2_POSE_STREAM", "MD2_DOWN_STREAM",
-                                    "MD2_DEC_WGRAD_STREAM"])
+                                    "MD2_DEC_WGRAD_STREAM", "MD2_ENC_WGRAD_STREAM"])
 @pytest.mark.parametrize("B,H,W", [(12, 128, 416), (2, 64, 128)])
 def test_fused_splitk_bn_bitwise(B, H, W, switch):
     import md2hip.dist
