@@ -27,7 +27,9 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 1
+/* Bumped on every change to an exported struct layout or signature.  2: md2_loss_out gained
+ * vis_cell; md2_model_cfg gained embedding_levels and num_bins.  Bindings refuse a mismatch. */
+#define MD2_ABI_VERSION 2
 
 #define MD2_OK 0
 #define MD2_EINVAL 1

@@ -22,6 +22,13 @@ import Flux
 const lib = get(ENV, "MD2HIP_LIB",
                 joinpath(@__DIR__, "..", "monodepth2.jl_amd", "lib", "libmd2hip.so"))
 
+const ABI_VERSION = 2                                  # include/md2.h MD2_ABI_VERSION
+function __init__()
+    v = ccall((:md2_abi_version, lib), Cint, ())
+    v == ABI_VERSION || error("libmd2hip at ", lib, " has ABI version ", v,
+                              ", MD2HIP.jl expects ", ABI_VERSION, ": rebuild or update the binding")
+end
+
 check(rc) = rc == 0 || error("libmd2hip (", rc, "): ",
                              unsafe_string(ccall((:md2_last_error, lib), Cstring, ())))
 stream_ptr() = AMDGPU.stream().stream                  # hipStream_t of the task-local stream

@@ -12,6 +12,7 @@
 // for every bucket before ADAM applies 1/nranks.
 #include <dlfcn.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -38,7 +39,19 @@ int rccl(Rccl** out) {
   static bool tried = false;
   if (!tried) {
     tried = true;
+    // MD2_RCCL_LIB swaps in the tests' call-recording stand-in (tests/stubs/rccl_stub.cpp).  A
+    // production run that inherited it would silently not reduce across ranks, so it is honoured
+    // only together with MD2_TUNING=1 (the test-and-tuning gate) and announced on stderr.
     const char* over = std::getenv("MD2_RCCL_LIB");
+    const char* tun = std::getenv("MD2_TUNING");
+    if (over && *over) {
+      if (tun && std::strcmp(tun, "1") == 0) {
+        std::fprintf(stderr, "libmd2hip: MD2_RCCL_LIB=%s replaces librccl (test stand-in)\n", over);
+      } else {
+        std::fprintf(stderr, "libmd2hip: ignoring MD2_RCCL_LIB=%s (needs MD2_TUNING=1)\n", over);
+        over = nullptr;
+      }
+    }
     const char* names[] = {over, "librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
     for (const char* n : names)
       if (n && *n && (r.h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;

@@ -1166,11 +1166,33 @@ __global__ __launch_bounds__(256) void plane_sum_kernel(const float* __restrict_
   *dst = s;
 }
 
+// the same block sum one pixel per thread, for maps whose h*w is not a multiple of 4 (e.g. the
+// 3x10 level-4 map of a 96x320 input)
+__global__ __launch_bounds__(256) void plane_sum1_kernel(const float* __restrict__ in, int P, int Cin,
+                                                         int C, int hw, float* __restrict__ out,
+                                                         int acc, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int q = (int)(i % hw);
+  const long t = i / hw;
+  const int c = (int)(t % C);
+  const long b = t / C;
+  const float* src = in + ((b * P) * Cin + c) * (long)hw + q;
+  float s = src[0];
+  for (int p = 1; p < P; ++p) s += src[(long)p * Cin * hw];
+  if (acc) s += out[i];
+  out[i] = s;
+}
+
 int plane_sum(const float* in, int N, int P, int Cin, int C, long hw, float* out, int accumulate,
               hipStream_t st) {
   if (hw % 4 != 0) {
-    set_error("plane_sum: h*w must be a multiple of 4");
-    return MD2_EINVAL;
+    const long n = (long)N * C * hw;
+    MD2_TRY(check_u31(n));
+    hipLaunchKernelGGL(plane_sum1_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, in, P, Cin, C, (int)hw,
+                       out, accumulate, n);
+    MD2_LAUNCH_CHECK();
+    return MD2_OK;
   }
   const long n4 = (long)N * C * (hw / 4);
   MD2_TRY(check_u31(4 * n4));

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <thread>
 #include <vector>
@@ -62,7 +63,13 @@ bool read_file(const char* path, std::vector<unsigned char>& buf, std::string& e
   return true;
 }
 
-bool decode_png(const char* path, Png& out, std::string& err) {
+// Largest image side accepted (KITTI is 1241x376, a Depth10k triplet 1248x128): a corrupt or
+// hostile header must not size an allocation.
+constexpr unsigned kMaxSide = 1u << 14;
+
+// exp_w / exp_h > 0: the caller's expected size, checked against IHDR before anything is
+// allocated.
+bool decode_png(const char* path, Png& out, std::string& err, int exp_w = 0, int exp_h = 0) {
   std::vector<unsigned char> f;
   if (!read_file(path, f, err)) return false;
   static const unsigned char sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
@@ -84,8 +91,22 @@ bool decode_png(const char* path, Png& out, std::string& err) {
       break;
     }
     if (!std::memcmp(type, "IHDR", 4)) {
-      out.w = (int)be32(data);
-      out.h = (int)be32(data + 4);
+      if (zinit || len != 13) {
+        err = std::string(zinit ? "repeated IHDR in " : "bad IHDR length in ") + path;
+        break;
+      }
+      const unsigned w = be32(data), h = be32(data + 4);
+      if (w == 0 || h == 0 || w > kMaxSide || h > kMaxSide) {
+        err = std::string("PNG size out of range (") + std::to_string(w) + "x" + std::to_string(h) + "): " + path;
+        return false;
+      }
+      out.w = (int)w;
+      out.h = (int)h;
+      if ((exp_w > 0 && out.w != exp_w) || (exp_h > 0 && out.h != exp_h)) {
+        err = std::string(path) + ": expected " + std::to_string(exp_w) + "x" + std::to_string(exp_h) + ", got " +
+              std::to_string(out.w) + "x" + std::to_string(out.h);
+        return false;
+      }
       depth = data[8];
       ctype = data[9];
       interlace = data[12];
@@ -198,7 +219,17 @@ int parallel_for(int n, int threads, F fn) {
   auto work = [&](int t) {
     for (int i; (i = next.fetch_add(1)) < n && !failed.load();) {
       std::string e;
-      if (!fn(i, e)) {
+      bool ok;
+      try {                            // nothing may escape a worker thread or the C ABI
+        ok = fn(i, e);
+      } catch (const std::exception& x) {
+        e = std::string("loader: ") + x.what();
+        ok = false;
+      } catch (...) {
+        e = "loader: unknown exception";
+        ok = false;
+      }
+      if (!ok) {
         errs[t] = e;
         failed.store(1);
       }
@@ -251,7 +282,7 @@ int md2_load_triplets_u8(const char* const* paths, int n, int width, int height,
   const size_t plane = (size_t)width * height, sample = 3 * 3 * plane;
   return parallel_for(n, threads, [&](int i, std::string& err) {
     Png p;
-    if (!decode_png(paths[i], p, err)) return false;
+    if (!decode_png(paths[i], p, err, 3 * width, height)) return false;
     if (p.w != 3 * width || p.h != height || p.ch < 3) {
       err = std::string(paths[i]) + ": expected a " + std::to_string(3 * width) + "x" + std::to_string(height) +
             " RGB triplet, got " + std::to_string(p.w) + "x" + std::to_string(p.h) + "x" + std::to_string(p.ch);

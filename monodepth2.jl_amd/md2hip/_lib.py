@@ -11,6 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MD2HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmd2hip.so"))
 
 MAX_SCALES = 5
+ABI_VERSION = 2          # include/md2.h MD2_ABI_VERSION: the struct layouts below
 
 
 class LossCfg(C.Structure):
@@ -175,6 +176,10 @@ def lib():
         f = getattr(l, name)
         f.restype = res
         f.argtypes = args
+    got = l.md2_abi_version()
+    if got != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH} has ABI version {got}, this binding expects {ABI_VERSION}: "
+                           "rebuild the library or update md2hip")
     _lib = l
     return l
 

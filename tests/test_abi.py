@@ -25,6 +25,6 @@ def test_library_exports_all_symbols():
     missing = [s for s in declared_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     lib.md2_abi_version.restype = ctypes.c_int
-    assert lib.md2_abi_version() == 1
+    assert lib.md2_abi_version() == 2
     lib.md2_last_error.restype = ctypes.c_char_p
     assert lib.md2_last_error() is not None

@@ -285,3 +285,42 @@ def test_native_batches_match_python_path(dtk, tmp_path):
     loader = md2hip.DataLoader(ds, 2, shuffle=True, seed=5, workers=4)
     for b, x in zip(loader.batch_indices(0), loader):
         np.testing.assert_array_equal(x.numpy(), np.stack([ds.getobs(i, seed=5) for i in b]))
+
+
+def test_native_png_decoder_rejects_corrupt_headers(tmp_path):
+    """truncated data, a repeated IHDR, a short IHDR, an absurd size and a size other
+    than the caller's all fail with an error naming the file (never a crash or an allocation sized
+    by the header)."""
+    import ctypes as C
+    import struct
+    import zlib
+    from md2hip._lib import lib
+    rng = np.random.default_rng(3)
+    rgb = rng.integers(0, 256, (16, 60, 3), dtype=np.uint8)
+    good = tmp_path / "good.png"
+    _write_png_filters(str(good), rgb)
+    blob = good.read_bytes()
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xffffffff)
+    sig, ihdr_end = blob[:8], 8 + 25
+    ihdr = blob[8:ihdr_end]
+    cases = {
+        "trunc.png": blob[:len(blob) // 2],                                   # IDAT cut short
+        "dup.png": sig + ihdr + ihdr + blob[ihdr_end:],                       # second IHDR
+        "short.png": sig + chunk(b"IHDR", ihdr[8:8 + 10]) + blob[ihdr_end:],  # 10-byte IHDR
+        "huge.png": sig + chunk(b"IHDR", struct.pack(">IIBBBBB", 0x80000000, 0x7fffffff, 8, 2, 0, 0, 0))
+                    + blob[ihdr_end:],
+        "size.png": None,                                                     # valid, wrong size
+    }
+    other = rng.integers(0, 256, (16, 63, 3), dtype=np.uint8)
+    _write_png_filters(str(tmp_path / "size.png"), other)
+    out = np.empty((1, 3, 3, 16, 20), dtype=np.uint8)
+    for name, data in cases.items():
+        if data is not None:
+            (tmp_path / name).write_bytes(data)
+        paths = (C.c_char_p * 1)(str(tmp_path / name).encode())
+        assert lib().md2_load_triplets_u8(paths, 1, 20, 16, None, C.c_void_p(out.ctypes.data), 1) != 0, name
+        assert name.encode() in lib().md2_last_error(), (name, lib().md2_last_error())
+    paths = (C.c_char_p * 1)(str(good).encode())
+    assert lib().md2_load_triplets_u8(paths, 1, 20, 16, None, C.c_void_p(out.ctypes.data), 1) == 0

@@ -213,7 +213,7 @@ def test_library_bucket_allreduce_order_with_recording_stub():
     import subprocess
     import sys
     root, so = _stub_lib()
-    env = dict(os.environ, MD2_RCCL_LIB=so)
+    env = dict(os.environ, MD2_RCCL_LIB=so, MD2_TUNING="1")
     r = subprocess.run([sys.executable, "-c", _STUB_CHILD, root], env=env, capture_output=True,
                        text=True, timeout=170)
     assert r.returncode == 0 and "STUB_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

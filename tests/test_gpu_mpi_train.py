@@ -14,8 +14,11 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("H,W,nb", [(64, 128, 4), (128, 416, 32)], ids=["64x128-4planes", "416x128-32planes"])
+@pytest.mark.parametrize("H,W,nb", [(64, 128, 4), (96, 320, 4), (128, 416, 32)],
+                         ids=["64x128-4planes", "96x320-4planes", "416x128-32planes"])
 def test_mpi_train_step_parity(H, W, nb):
+    """96x320: the level-4 map is 3x10 = 30 pixels, not a multiple of 4 -- the _repeat pullback
+    takes its one-pixel-per-thread path."""
     from tests._model_parity import check_step, oracle_bounds, run
     g, o, errs = run(N=1, H=H, W=W, sources="texture", num_bins=nb)
     assert len(g["disps"]) == 4 and g["disps"][-1].shape == (nb, 1, H, W)

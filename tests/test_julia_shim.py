@@ -185,3 +185,16 @@ def test_train_loss_return_convention(sources):
     assert re.search(r"Flux\.trainable\(m::HIPModel\) = \(θ = m\.θ,\)", jl)
     # after an update of θ outside the library the packed weights are refreshed before use
     assert "m.packed || repack!(m)" in body
+
+
+def test_abi_version_pinned_in_every_binding():
+    """The header's MD2_ABI_VERSION is what both bindings refuse to run without."""
+    hdr = open(HDR).read()
+    v = int(re.search(r"#define MD2_ABI_VERSION (\d+)", hdr).group(1))
+    jl = open(JL).read()
+    assert int(re.search(r"const ABI_VERSION = (\d+)", jl).group(1)) == v
+    assert "function __init__()" in jl and "md2_abi_version" in jl
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "monodepth2.jl_amd"))
+    from md2hip import _lib
+    assert _lib.ABI_VERSION == v
