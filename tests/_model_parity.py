@@ -14,6 +14,10 @@ Source frames (``sources``):
   "ramp"     affine ramps (bilinear sampling of them has no kinks at all),
   "texture"  low-frequency texture + 15 % pixel noise (tests/_data.py),
   "uniform"  the bench's own i.i.d. U[0,1) triplets (md2hip.dist.synthetic_triplets)."""
+import json
+import os
+import re
+
 import torch
 
 import md2hip
@@ -227,14 +231,46 @@ def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_i
             "bwd": per_tensor(spec, g["grad"].double(), s64)}
 
 
+# Absolute ceilings on the adaptive bounds below: whatever the oracle's own
+# sensitivity says, no tensor may be further than this from the reference.
+CEIL_BWD = 1e-4          # backward at the GPU's own forward point
+CEIL_E2E = 1e-3          # end to end vs the fp64 oracle
+# Named exceptions: tensors whose gradient is a cancelling sum over every pixel of a level, so its
+# relative error is the pixel gradients' fp32 rounding divided by the cancellation factor (10-1000x,
+# DESIGN.md section 2 "coherent rounding").  They keep the adaptive bound and a looser ceiling.
+CEIL_EXCEPT = {
+    r"^depth\.head\d\.bias$": (1e-3, 1e-2),   # disparity-head bias: sum of ~1e6 signed pixel gradients
+}
+
+
+def _ceilings(name):
+    for pat, c in CEIL_EXCEPT.items():
+        if re.match(pat, name):
+            return c
+    return CEIL_BWD, CEIL_E2E
+
+
+def parity_record_path(label):
+    """Where check_step writes its per-tensor record: $MD2_PARITY_DIR (default gpurun_out/parity,
+    which gpurun pulls back from the box)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = os.environ.get("MD2_PARITY_DIR", os.path.join(root, "gpurun_out", "parity"))
+    os.makedirs(d, exist_ok=True)
+    return os.path.join(d, re.sub(r"[^A-Za-z0-9_.-]+", "_", label or "step") + ".json")
+
+
 def check_step(g, o, errs, b, label=""):
     """The full-step assertions shared by the model parity tests (b = oracle_bounds(g, o)):
       * loss within max(1e-6, 4 x its fp32 floor); disparities / poses within max(1e-5, 4 x floor);
       * BACKWARD, per tensor: |gpu - sub| within max(4 x the backward's fp32 floor, 4 x its coherent
         warp-constant sensitivity, 2e-5) -- the GPU reproduces the exact gradient at its own
-        forward point;
+        forward point -- and never above CEIL_BWD (1e-4);
       * END TO END, per tensor: |gpu - oracle| within max(4 x the fp32 floor, 2 x what the
-        forward's rounding explains, the backward bound + what the forward explains, 2e-5)."""
+        forward's rounding explains, the backward bound + what the forward explains, 2e-5), and
+        never above CEIL_E2E (1e-3).  CEIL_EXCEPT names the cancelling-sum tensors that get looser
+        ceilings.
+    Every tensor's (err, bound, floor, explained, coherent) is written to parity_record_path(label)
+    before anything is asserted."""
     floor = b["floor"]
     assert abs(g["loss"] - o["loss"]) <= max(1e-6, 4 * floor["__loss"]) * abs(o["loss"]), \
         (g["loss"], o["loss"], floor["__loss"])
@@ -244,6 +280,19 @@ def check_step(g, o, errs, b, label=""):
     bb = {k: max(4 * b["floor_b"][k], 4 * b["coherent"][k], 2e-5) for k in b["bwd"]}
     # end to end <= backward error + what the forward's rounding explains (triangle inequality)
     be = {k: max(4 * floor[k], 2 * b["explained"][k], bb[k] + b["explained"][k], 2e-5) for k in errs}
+    rec = {"label": label, "loss_gpu": g["loss"], "loss_oracle": o["loss"],
+           "loss_rel_err": abs(g["loss"] - o["loss"]) / abs(o["loss"]), "loss_floor": floor["__loss"],
+           "disp_rel_err": [D.rel_err(a, r) for a, r in zip(g["disps"], o["disps"])],
+           "pose_rel_err": D.rel_err(g["pose"], o["pose"]),
+           "ceilings": {"backward": CEIL_BWD, "end_to_end": CEIL_E2E, "except": CEIL_EXCEPT},
+           "tensors": {k: {"bwd_err": b["bwd"][k], "bwd_bound": bb[k], "bwd_ceiling": _ceilings(k)[0],
+                           "e2e_err": errs[k], "e2e_bound": be[k], "e2e_ceiling": _ceilings(k)[1],
+                           "floor": floor[k], "floor_b": b["floor_b"][k], "explained": b["explained"][k],
+                           "coherent": b["coherent"][k]} for k in errs}}
+    rec["worst_bwd"] = max(rec["tensors"].items(), key=lambda kv: kv[1]["bwd_err"])[0]
+    rec["worst_e2e"] = max(rec["tensors"].items(), key=lambda kv: kv[1]["e2e_err"])[0]
+    with open(parity_record_path(label), "w") as f:
+        json.dump(rec, f, indent=1)
     rb = sorted(((b["bwd"][k] / bb[k], k) for k in bb), reverse=True)
     re_ = sorted(((errs[k] / be[k], k) for k in be), reverse=True)
     print(f"\n{label} loss {g['loss']:.7f} vs {o['loss']:.7f}; backward (gpu vs oracle at gpu outputs): " +
@@ -255,4 +304,8 @@ def check_step(g, o, errs, b, label=""):
     assert not bad, ("backward", bad)
     bad = {k: (errs[k], be[k]) for k in be if errs[k] > be[k]}
     assert not bad, ("end to end", bad)
+    bad = {k: (b["bwd"][k], _ceilings(k)[0]) for k in bb if b["bwd"][k] > _ceilings(k)[0]}
+    assert not bad, ("backward above the absolute ceiling", bad)
+    bad = {k: (errs[k], _ceilings(k)[1]) for k in errs if errs[k] > _ceilings(k)[1]}
+    assert not bad, ("end to end above the absolute ceiling", bad)
     return max(errs.values())

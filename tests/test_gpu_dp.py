@@ -9,7 +9,10 @@
 3. World size 2, both ranks on cuda:0 with the real executor (gloo control plane, host-staged
    bucket reduce): the reduced gradient equals the sum of the two shard gradients computed
    sequentially, bit for bit, and both ranks end with identical parameters.  BatchNorm
-   statistics are per shard, as designed (no SyncBN; the reference is single-device)."""
+   statistics are per shard, as designed (no SyncBN; the reference is single-device).  Run at a
+   small shape and at the per-rank workloads of BASELINE configs 4 (ResNet-18 416x128, 12
+   triplets per rank) and 5 (ResNet-50 640x192, 8 per rank) -- scripts/script.jl:84-86.
+4. The bucket order through a call-recording RCCL stand-in, at the small and the config-4 shape."""
 import os
 import socket
 
@@ -23,26 +26,34 @@ pytestmark = pytest.mark.gpu
 H, W = 64, 128
 
 
-def _model(seed=42):
+# (arch, H, W, triplets per rank)
+SHAPES = {"r18-64x128-b2": (18, 64, 128, 2),
+          "config4-r18-416x128-b12": (18, 128, 416, 12),
+          "config5-r50-640x192-b8": (50, 192, 640, 8)}
+
+
+def _model(seed=42, arch=18):
     import md2hip
-    enc = md2hip.ResNet(18, in_channels=3)
+    enc = md2hip.ResNet(arch, in_channels=3)
     return md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
                                                  embedding_levels=0), md2hip.PoseDecoder(512), seed=seed)
 
 
-def _setup(model, N):
+def _setup(model, N, h=H, w=W):
     import md2hip
-    K, invK = md2hip.depth10k_intrinsics(W, H)
+    K, invK = md2hip.depth10k_intrinsics(w, h)
     cache = md2hip.TrainCache(K=K, invK=invK)
-    params = md2hip.Params(target_size=(W, H), batch_size=N, automasking=False)
-    return model.executor((N, 3, 3, H, W), cache, params)
+    params = md2hip.Params(target_size=(w, h), batch_size=N, automasking=False)
+    return model.executor((N, 3, 3, h, w), cache, params)
 
 
-def test_backward_buckets_final_when_segment_returns():
+@pytest.mark.parametrize("shape", list(SHAPES), ids=list(SHAPES))
+def test_backward_buckets_final_when_segment_returns(shape):
     from md2hip.dist import synthetic_triplets
-    m = _model()
-    ex = _setup(m, 2)
-    x = synthetic_triplets(2, H, W, 0, "cuda")
+    arch, h, w, per = SHAPES[shape]
+    m = _model(arch=arch)
+    ex = _setup(m, per, h, w)
+    x = synthetic_triplets(per, h, w, 0, "cuda")
     m.grad.fill_(float("nan"))
     ex.forward_loss(x)
     snaps = []
@@ -90,7 +101,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _dp_worker(rank, world, port, q):
+def _dp_worker(rank, world, port, q, shape):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (root, os.path.join(root, "monodepth2.jl_amd")):
@@ -104,10 +115,10 @@ def _dp_worker(rank, world, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        per = 2
-        x = MD.synthetic_triplets(per, H, W, rank * per, "cuda")
-        m = _model()
-        ex = _setup(m, per)
+        arch, h, w, per = shape
+        x = MD.synthetic_triplets(per, h, w, rank * per, "cuda")
+        m = _model(arch=arch)
+        ex = _setup(m, per, h, w)
         # this shard's own gradient (no exchange)
         ex.forward_loss(x)
         ex.backward()
@@ -122,18 +133,19 @@ def _dp_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(240)
-def test_world2_same_device_reduced_gradient_is_shard_sum():
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("shape", list(SHAPES), ids=list(SHAPES))
+def test_world2_same_device_reduced_gradient_is_shard_sum(shape):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, SHAPES[shape])) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(2):
-        r, local, reduced, flat = q.get(timeout=200)     # numpy: no fd sharing with the child
+        r, local, reduced, flat = q.get(timeout=260)     # numpy: no fd sharing with the child
         res[r] = (torch.from_numpy(local), torch.from_numpy(reduced), torch.from_numpy(flat))
     for p in procs:
         p.join(timeout=60)
@@ -151,12 +163,13 @@ sys.path[:0] = [root, os.path.join(root, "monodepth2.jl_amd")]
 import torch, md2hip
 from md2hip import comm as MC
 from md2hip.dist import synthetic_triplets
-from tests.test_gpu_dp import _model, _setup, H, W
+from tests.test_gpu_dp import _model, _setup, SHAPES
+arch, H, W, per = SHAPES[sys.argv[2]]
 stub = C.CDLL(os.environ["MD2_RCCL_LIB"])
 stub.stub_get.argtypes = [C.c_int] + [C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
-m = _model()
-ex = _setup(m, 2)
-x = synthetic_triplets(2, H, W, 0, "cuda")
+m = _model(arch=arch)
+ex = _setup(m, per, H, W)
+x = synthetic_triplets(per, H, W, 0, "cuda")
 dev = torch.cuda.current_device()
 c = MC.Comm(0, 2, bytes(128), 0)                     # "world 2": the stub never reduces
 assert torch.cuda.current_device() == dev
@@ -203,7 +216,8 @@ def _stub_lib():
 
 
 @pytest.mark.timeout(180)
-def test_library_bucket_allreduce_order_with_recording_stub():
+@pytest.mark.parametrize("shape", ["r18-64x128-b2", "config4-r18-416x128-b12"])
+def test_library_bucket_allreduce_order_with_recording_stub(shape):
     """md2_model_backward_allreduce through a call-recording RCCL stand-in (tests/stubs): ONE
     collective per backward segment, in segment order, each covering exactly that segment's final
     gradient range, all on the communicator's own stream (not the caller's), and each ordered
@@ -214,6 +228,6 @@ def test_library_bucket_allreduce_order_with_recording_stub():
     import sys
     root, so = _stub_lib()
     env = dict(os.environ, MD2_RCCL_LIB=so, MD2_TUNING="1")
-    r = subprocess.run([sys.executable, "-c", _STUB_CHILD, root], env=env, capture_output=True,
+    r = subprocess.run([sys.executable, "-c", _STUB_CHILD, root, shape], env=env, capture_output=True,
                        text=True, timeout=170)
     assert r.returncode == 0 and "STUB_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

@@ -133,4 +133,10 @@ def test_slow_depth_trajectory(textured_theta):
         assert cos > 0.99, cos.item()
         pg = sd.pose_rows.detach().double().cpu() - rows
         po = torch.cat([torch.cat([r, t], 1) for r, t in zip(rv, tv)], 0) - rows
+        import json
+        from tests._model_parity import parity_record_path
+        per = (pg - po).abs() / po.abs().clamp_min(1e-30)
+        with open(parity_record_path("slow_depth_trajectory"), "w") as f:
+            json.dump({"loss_gpu": gl, "loss_oracle": ol, "disp_update_cos": cos.item(),
+                       "pose_update_rel_err": D.rel_err(pg, po), "pose_update_per_entry": per.tolist()}, f, indent=1)
         assert D.rel_err(pg, po) < 2e-2

@@ -2,7 +2,10 @@
 bucket of the RCCL all-reduce, md2_model_backward_allreduce) its gradient bytes, its own
 backward time, and the backward time still REMAINING after it (the window its all-reduce can hide
 in), against that bucket's ring all-reduce time at 8 ranks for assumed RCCL bus bandwidths.
-    python tools/dp_overlap.py [OUT.json]"""
+    python tools/dp_overlap.py [OUT.json] [--arch 18|50 --height H --width W --batch B]
+Defaults: BASELINE config 4's per-rank workload (ResNet-18 416x128, 12 triplets); config 5 is
+--arch 50 --height 192 --width 640 --batch 8."""
+import argparse
 import json
 import os
 import sys
@@ -14,12 +17,19 @@ import torch  # noqa: E402
 import md2hip  # noqa: E402
 from md2hip.dist import synthetic_triplets  # noqa: E402
 
-B, H, W, RANKS = 12, 128, 416, 8
+ap = argparse.ArgumentParser()
+ap.add_argument("out", nargs="?")
+ap.add_argument("--arch", type=int, default=18)
+ap.add_argument("--height", type=int, default=128)
+ap.add_argument("--width", type=int, default=416)
+ap.add_argument("--batch", type=int, default=12)
+args = ap.parse_args()
+B, H, W, RANKS = args.batch, args.height, args.width, 8
 BUSBW = (150.0, 300.0, 600.0)     # GB/s: one xGMI link .. RCCL multi-channel over the 7 links
 LAT_US = 25.0                     # per-collective latency assumed for small buckets
 names = ["pose+depth decoders", "layer4", "layer3", "layer2", "layer1", "stem"]
 
-enc = md2hip.ResNet(18, in_channels=3)
+enc = md2hip.ResNet(args.arch, in_channels=3)
 model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
                                               embedding_levels=0), md2hip.PoseDecoder(512), seed=42)
 K, invK = md2hip.depth10k_intrinsics(W, H)
@@ -43,7 +53,7 @@ for it in range(8):
         samples.append([ev[k + 1].elapsed_time(ev[k + 2]) for k in range(ex.nseg)] + [ev[0].elapsed_time(ev[1])])
 med = [sorted(s[k] for s in samples)[len(samples) // 2] for k in range(ex.nseg + 1)]
 seg_ms, fwd_ms = med[:ex.nseg], med[ex.nseg]
-out = {"batch_per_gpu": B, "size": [W, H], "ranks": RANKS, "forward_ms": fwd_ms,
+out = {"arch": args.arch, "batch_per_gpu": B, "size": [W, H], "ranks": RANKS, "forward_ms": fwd_ms,
        "backward_ms": sum(seg_ms), "busbw_GBps": BUSBW, "latency_us": LAT_US, "buckets": []}
 for k, (off, ln) in enumerate(rng):
     bytes_ = 4 * ln
@@ -63,6 +73,6 @@ for b in map(str, BUSBW):
         t_free = max(t_free, t_seg_end) + out["buckets"][k]["allreduce_ms"][b]
     out.setdefault("exposed_ms", {})[b] = max(0.0, t_free - t_seg_end)
 print(json.dumps(out, indent=1))
-if len(sys.argv) > 1:
-    with open(sys.argv[1], "w") as f:
+if args.out:
+    with open(args.out, "w") as f:
         json.dump(out, f, indent=1)
