@@ -534,27 +534,41 @@ int strip_rows(const ConvShape& s) { return strip_units(s, 16) >= 512 ? 16 : 8; 
 int strip_cpw(int Cin) { return Cin >= 32 ? 8 : 4; }
 
 // ---------------------------------------------------------------------------------------------
-// Batched heads: every block first finds its head (a linear scan over <= MAX_HEADS prefix
-// offsets), then runs the strip body of the single-head kernels above with reflect padding.
+// Batched heads (all disparity heads of the DepthDecoder in one launch per pass).  Every head is
+// an HBM pass over its Cin input planes (9*Cin MACs per pixel), so the kernels are shaped for
+// bytes: a lane owns V = 4 (2 when W % 4 != 0) consecutive pixels of one row and moves them as
+// ONE float4 (float2) load / store; the +-1 column neighbours come from the adjacent lanes by DPP.
+// A wave covers 62 consecutive pixel vectors of the flattened [image][row][vector] index space:
+// lanes 0 and 63 are halo loaders only (their vectors belong to the neighbouring tiles), so the
+// DPP neighbour of every owning lane is always loaded, with no divergent edge loads.  Where a
+// row starts or ends inside the wave the column taps fold by reflection (pad_reflect excludes the
+// edge, src/depth_decoder.jl:5) from the lane's own vector.
+//   forward   block = one 62-vector tile; wave q of the block sums channel quarter q; the four
+//             partial sums are added in wave order through LDS, then bias + sigmoid.
+//   backward  ONE pass per (head, 4-channel chunk, run of T tiles) wave item: the 9 tap-shifted
+//             dy values D of each pixel (with the reflect folds) are formed once per tile, then
+//             per channel dx = w . D is stored and the filter-gradient sums dy * x(window) are
+//             accumulated; at the end of the run they are wave-summed into one partial row.
+//             The bias gradient (sum of dy, a long cancelling sum) stays fp64.  A fixed-order
+//             column reduction finishes dw / db.
 // ---------------------------------------------------------------------------------------------
-constexpr int HB_FR = 8;    // forward rows per strip unit
-constexpr int HB_DR = 4;    // data-gradient rows per wave unit
-constexpr int HB_WR = 8;    // filter-gradient rows per strip unit (16 measured slower: 62 vs 46 us)
-constexpr int HB_CPW = 4;   // filter-gradient channels per wave (16 per block)
+constexpr int HB_TILE = 62;   // owned pixel vectors per wave (lanes 1..62)
+constexpr int HB_CH = 2;      // filter gradient: channels per wave item (4: 193 VGPRs)
+constexpr int HB_DCH = 16;    // data gradient: channels per wave item
 
 struct HeadBatch {
   HeadJob j[MAX_HEADS];
   int n, act;
-  long u0[MAX_HEADS + 1];   // forward: first block of each head
-  long d0[MAX_HEADS + 1];   // data gradient: first block (4 wave units per block)
-  long w0[MAX_HEADS + 1];   // filter gradient: first block
-  long c0[MAX_HEADS + 1];   // filter gradient: first reduction column
-  long p0[MAX_HEADS];       // filter gradient: first partial (float offset of the head's rows)
-  long b0[MAX_HEADS];       // filter gradient: first bias partial (fp64, after all float rows)
-  int G[MAX_HEADS];         // data gradient: channel groups
-  int FR[MAX_HEADS];        // forward: rows per strip unit (<= HB_FR; fewer on the deep coarse heads)
-  int WR[MAX_HEADS];        // filter gradient: rows per strip unit (<= HB_WR)
-  int CB[MAX_HEADS];        // filter gradient: channel blocks of 4*HB_CPW
+  int V[MAX_HEADS];          // pixels per lane
+  long ntile[MAX_HEADS];     // 62-vector tiles of the head
+  long f0[MAX_HEADS + 1];    // forward: first block of each head
+  int T[MAX_HEADS];          // backward: tiles per wave item
+  int nrun[MAX_HEADS];       // backward: runs of T tiles
+  long d0[MAX_HEADS + 1];    // data gradient: first wave item of each head
+  long w0[MAX_HEADS + 1];    // filter gradient: first wave item of each head
+  long c0[MAX_HEADS + 1];    // reduction: first column of each head
+  long p0[MAX_HEADS];        // partial rows [nrun][Cin*9] (float offset)
+  long q0[MAX_HEADS];        // fp64 bias partials [nrun] (double offset, after every float row)
 };
 
 __device__ __forceinline__ int hb_find(const long* off, int n, long b) {
@@ -562,222 +576,314 @@ __device__ __forceinline__ int hb_find(const long* off, int n, long b) {
   while (k + 1 < n && b >= off[k + 1]) ++k;
   return k;
 }
-__device__ __forceinline__ StripGeo hb_geo(const HeadJob& j, int R) {
-  StripGeo g;
-  g.H = j.H;
-  g.W = j.W;
-  g.nseg = (j.W + 63) / 64;
-  g.nband = (j.H + R - 1) / R;
-  return g;
+
+template <int V> struct VecT;
+template <> struct VecT<4> { using T = float4; };
+template <> struct VecT<2> { using T = float2; };
+
+template <int V>
+__device__ __forceinline__ void vload(const float* p, float (&v)[V]) {
+  const auto t = *reinterpret_cast<const typename VecT<V>::T*>(p);
+  v[0] = t.x;
+  v[1] = t.y;
+  if constexpr (V == 4) {
+    v[2] = t.z;
+    v[3] = t.w;
+  }
+}
+template <int V>
+__device__ __forceinline__ void vstore(float* p, const float (&v)[V]) {
+  if constexpr (V == 4)
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  else
+    *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
 }
 
-__global__ __launch_bounds__(256) void heads_fwd_kernel(HeadBatch hb) {
-  constexpr int R = HB_FR;
-  __shared__ float s_part[3][R][64];
-  const int k = hb_find(hb.u0, hb.n, blockIdx.x);
-  const HeadJob& J = hb.j[k];
-  const int Rk = hb.FR[k];
-  const StripGeo g = hb_geo(J, Rk);
+__device__ __forceinline__ float hb_from_left(float v) {    // lane i <- lane i-1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float hb_from_right(float v) {   // lane i <- lane i+1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
+}
+
+// The lane's pixel vector: tile t, lane -> flat vector g = 62 t + lane - 1 (clamped into range
+// for the loads; `own` = a lane that owns a real vector)
+struct HbPix {
+  int b, y, cx;
+  bool own;
+};
+template <int V>
+__device__ __forceinline__ HbPix hb_pix(const HeadJob& J, long t, int lane) {
+  const int Wv = J.W / V;
+  const long nv = (long)J.N * J.H * Wv;
+  long g = t * HB_TILE + lane - 1;
+  HbPix p;
+  p.own = lane >= 1 && lane <= HB_TILE && g >= 0 && g < nv;
+  g = g < 0 ? 0 : (g >= nv ? nv - 1 : g);
+  const long r = g / Wv;
+  p.cx = (int)(g - r * Wv);
+  p.b = (int)(r / J.H);
+  p.y = (int)(r - (long)p.b * J.H);
+  return p;
+}
+
+// row `row` of plane xc around the lane's vector: a[0] = column 4cx-1, a[1..V] = the vector,
+// a[V+1] = column 4cx+V, the outer two folded by reflection at the row ends (mirror excluding the
+// edge: -1 -> 1, W -> W-2)
+template <int V>
+__device__ __forceinline__ void hb_row_reflect(const float* __restrict__ xc, int row, int W, int cx, int Wv,
+                                               float (&a)[V + 2]) {
+  float v[V];
+  vload<V>(xc + (long)row * W + cx * V, v);
+  const float l = hb_from_left(v[V - 1]), r = hb_from_right(v[0]);
+#pragma unroll
+  for (int i = 0; i < V; ++i) a[i + 1] = v[i];
+  a[0] = cx == 0 ? v[1] : l;
+  a[V + 1] = cx == Wv - 1 ? v[V - 2] : r;
+}
+// the same with zero padding outside the row and a zero row outside the image (dy)
+template <int V>
+__device__ __forceinline__ void hb_row_zero(const float* __restrict__ g, int row, int H, int W, int cx, int Wv,
+                                            float (&a)[V + 2]) {
+  float v[V];
+  const bool in = row >= 0 && row < H;
+  vload<V>(g + (long)(in ? row : 0) * W + cx * V, v);
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] = in ? v[i] : 0.f;
+  const float l = hb_from_left(v[V - 1]), r = hb_from_right(v[0]);
+#pragma unroll
+  for (int i = 0; i < V; ++i) a[i + 1] = v[i];
+  a[0] = cx == 0 ? 0.f : l;
+  a[V + 1] = cx == Wv - 1 ? 0.f : r;
+}
+
+__device__ __forceinline__ int hb_reflect(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * n - 2 - i : i;
+}
+
+template <int V>
+__device__ void heads_fwd_body(const HeadBatch& hb, const HeadJob& J, long t, float (*s_part)[64][4]) {
   const int lane = threadIdx.x & 63, wq = threadIdx.x >> 6;
-  int b, y0, xx;
-  strip_unit(g, (int)(blockIdx.x - hb.u0[k]), Rk, b, y0, xx);
-  int co[3];
-  bool cv[3];
-  strip_cols<true>(xx, g.W, co, cv);
-  const long HW = (long)g.H * g.W;
-  const float* xb = J.x.p + img_off(J.x, b);
+  const HbPix p = hb_pix<V>(J, t, lane);
+  const int Wv = J.W / V;
+  const long HW = (long)J.H * J.W;
+  const int ym = hb_reflect(p.y - 1, J.H), yp = hb_reflect(p.y + 1, J.H);
+  const float* xb = J.x.p + img_off(J.x, p.b);
   const int cpw = (J.Cin + 3) >> 2;
   const int cb = wq * cpw, ce = min(J.Cin, cb + cpw);
-  float out[R];
+  float out[V];
 #pragma unroll
-  for (int r = 0; r < R; ++r) out[r] = 0.f;
-#pragma unroll 4
+  for (int i = 0; i < V; ++i) out[i] = 0.f;
+#pragma unroll 2
   for (int c = cb; c < ce; ++c) {
     const float* xc = xb + c * HW;
     float wt[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wt[t] = J.wf.p[(long)c * J.wf.sc + (long)t * J.wf.st];
-    float a0[3], a1[3], a2[3];
-    strip_row<true>(xc, y0 - 1, g.H, g.W, co, cv, a0);
-    strip_row<true>(xc, y0, g.H, g.W, co, cv, a1);
+    for (int q = 0; q < 9; ++q) wt[q] = J.wf.p[(long)c * J.wf.sc + (long)q * J.wf.st];
+    float a0[V + 2], a1[V + 2], a2[V + 2];
+    hb_row_reflect<V>(xc, ym, J.W, p.cx, Wv, a0);
+    hb_row_reflect<V>(xc, p.y, J.W, p.cx, Wv, a1);
+    hb_row_reflect<V>(xc, yp, J.W, p.cx, Wv, a2);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r >= Rk) break;
-      strip_row<true>(xc, y0 + r + 1, g.H, g.W, co, cv, a2);
-      float v = out[r];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        v = fmaf(wt[q], a0[q], v);
-        v = fmaf(wt[3 + q], a1[q], v);
-        v = fmaf(wt[6 + q], a2[q], v);
-      }
-      out[r] = v;
+    for (int i = 0; i < V; ++i) {
+      float v = out[i];
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        a0[q] = a1[q];
-        a1[q] = a2[q];
+        v = fmaf(wt[q], a0[i + q], v);
+        v = fmaf(wt[3 + q], a1[i + q], v);
+        v = fmaf(wt[6 + q], a2[i + q], v);
       }
+      out[i] = v;
     }
   }
   if (wq > 0) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) s_part[wq - 1][r][lane] = out[r];
+    for (int i = 0; i < V; ++i) s_part[wq - 1][lane][i] = out[i];
   }
   __syncthreads();
-  if (wq > 0 || xx >= g.W) return;
+  if (wq > 0 || !p.own) return;
   const float bb = J.bias ? J.bias[0] : 0.f;
+  float y[V];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if (r >= Rk || y0 + r >= g.H) break;
-    const float v = ((out[r] + s_part[0][r][lane]) + s_part[1][r][lane]) + s_part[2][r][lane];
-    J.y[(long)b * J.ybs + (long)(y0 + r) * g.W + xx] = act_f(v + bb, hb.act);
-  }
+  for (int i = 0; i < V; ++i)
+    y[i] = act_f(((out[i] + s_part[0][lane][i]) + s_part[1][lane][i]) + s_part[2][lane][i] + bb, hb.act);
+  vstore<V>(J.y + (long)p.b * J.ybs + (long)p.y * J.W + p.cx * V, y);
 }
 
-__global__ __launch_bounds__(256) void heads_dgrad_kernel(HeadBatch hb) {
-  constexpr int R = HB_DR;
-  const int k = hb_find(hb.d0, hb.n, blockIdx.x);
-  const HeadJob& J = hb.j[k];
-  const StripGeo g = hb_geo(J, R);
-  const long nunits = (long)J.N * g.nband * g.nseg;
-  const long wu = (blockIdx.x - hb.d0[k]) * 4 + (threadIdx.x >> 6);
-  if (wu >= nunits * hb.G[k]) return;                       // wave-uniform
-  const int grp = (int)(wu % hb.G[k]);
-  int b, y0, qx;
-  strip_unit(g, (int)(wu / hb.G[k]), R, b, y0, qx);
-  const long HW = (long)g.H * g.W;
-  const float* gb = J.dy + (long)b * HW;
-  float D[R][9];
-  float e0[3], e1[3], e2[3];
-  strip_erow<true>(gb, y0 + 1, g.H, g.W, qx, e0);
-  strip_erow<true>(gb, y0, g.H, g.W, qx, e1);
-  strip_erow<true>(gb, y0 - 1, g.H, g.W, qx, e2);
-  float ef0[3] = {0.f, 0.f, 0.f}, efH[3] = {0.f, 0.f, 0.f};
-  if (y0 <= 1 && 1 < y0 + R) strip_erow<true>(gb, 0, g.H, g.W, qx, ef0);
-  if (y0 <= g.H - 2 && g.H - 2 < y0 + R) strip_erow<true>(gb, g.H - 1, g.H, g.W, qx, efH);
+__global__ __launch_bounds__(256) void heads_fwd_kernel(HeadBatch hb) {
+  __shared__ float s_part[3][64][4];
+  const int k = hb_find(hb.f0, hb.n, blockIdx.x);
+  const long t = blockIdx.x - hb.f0[k];
+  if (hb.V[k] == 4)
+    heads_fwd_body<4>(hb, hb.j[k], t, s_part);
+  else
+    heads_fwd_body<2>(hb, hb.j[k], t, s_part);
+}
+
+// E(row) of the data gradient for pixel i at the three column taps kx (p.x = q.x + 1 - kx), from
+// the zero-padded row a (a[i+1] = column of pixel i), with the reflect folds in x: q = 1 also
+// takes p = 0 through kx = 0, q = W-2 takes p = W-1 through kx = 2
+template <int V>
+__device__ __forceinline__ void hb_erow(const float (&a)[V + 2], int cx, int Wv, float (&e)[3][V]) {
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int qy = y0 + r;
-    const bool f0 = qy == 1, fH = qy == g.H - 2;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      D[r][q] = e0[q] + (f0 ? ef0[q] : 0.f);
-      D[r][3 + q] = e1[q];
-      D[r][6 + q] = e2[q] + (fH ? efH[q] : 0.f);
-    }
-    if (r + 1 < R) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        e2[q] = e1[q];
-        e1[q] = e0[q];
-      }
-      strip_erow<true>(gb, qy + 2, g.H, g.W, qx, e0);
-    }
+  for (int i = 0; i < V; ++i) {
+    e[0][i] = a[i + 2];
+    e[1][i] = a[i + 1];
+    e[2][i] = a[i];
   }
-  if (qx >= g.W) return;
-  float* out = J.dx + (long)b * J.dxbs + (long)y0 * g.W + qx;
-  const int cpg = (J.Cin + hb.G[k] - 1) / hb.G[k];
-  const int cb = grp * cpg, ce = min(J.Cin, cb + cpg);
+  if (cx == 0) e[0][1] += a[1];
+  if (cx == Wv - 1) e[2][V - 2] += a[V];
+}
+
+// data gradient item: one 62-vector tile x HB_DCH channels.  D[ky][kx][i] = dy(q.y + 1 - ky,
+// q.x + 1 - kx) with the folds: q.y = 1 also takes p.y = 0 through ky = 0, q.y = H-2 takes
+// p.y = H-1 through ky = 2; then dx[c] = sum_tap w_d[c][tap] D[tap] for each channel.
+template <int V>
+__device__ void heads_dgrad_body(const HeadBatch& hb, int k, long item) {
+  const HeadJob& J = hb.j[k];
+  const int lane = threadIdx.x & 63;
+  const int nch = (J.Cin + HB_DCH - 1) / HB_DCH;
+  const int ch = (int)(item % nch);
+  const long t = item / nch;
+  const int Wv = J.W / V;
+  const long HW = (long)J.H * J.W;
+  const HbPix p = hb_pix<V>(J, t, lane);
+  const float* gb = J.dy + (long)p.b * HW;
+  float dm[V + 2], d0[V + 2], dp[V + 2];
+  hb_row_zero<V>(gb, p.y - 1, J.H, J.W, p.cx, Wv, dm);
+  hb_row_zero<V>(gb, p.y, J.H, J.W, p.cx, Wv, d0);
+  hb_row_zero<V>(gb, p.y + 1, J.H, J.W, p.cx, Wv, dp);
+  float D[3][3][V], Em[3][V];
+  hb_erow<V>(dp, p.cx, Wv, D[0]);
+  hb_erow<V>(d0, p.cx, Wv, D[1]);
+  hb_erow<V>(dm, p.cx, Wv, Em);
+  const bool f0 = p.y == 1, fH = p.y == J.H - 2;
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      D[2][q][i] = Em[q][i] + (fH ? D[0][q][i] : 0.f);
+      D[0][q][i] += f0 ? Em[q][i] : 0.f;
+    }
+  if (!p.own) return;
+  float* dxb = J.dx + (long)p.b * J.dxbs + (long)p.y * J.W + p.cx * V;
+  const int cb = ch * HB_DCH, ce = min(J.Cin, cb + HB_DCH);
+#pragma unroll 4
   for (int c = cb; c < ce; ++c) {
-    float wt[9];
+    float wd[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wt[t] = J.wd.p[(long)c * J.wd.sc + (long)t * J.wd.st];
+    for (int q = 0; q < 9; ++q) wd[q] = J.wd.p[(long)c * J.wd.sc + (long)q * J.wd.st];
+    float dx[V];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (y0 + r >= g.H) break;
+    for (int i = 0; i < V; ++i) {
       float v = 0.f;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) v = fmaf(wt[t], D[r][t], v);
-      out[c * HW + (long)r * g.W] = v;
+      for (int q = 0; q < 9; ++q) v = fmaf(wd[q], D[q / 3][q % 3][i], v);
+      dx[i] = v;
     }
+    vstore<V>(dxb + c * HW, dx);
   }
 }
 
-__global__ __launch_bounds__(256) void heads_wgrad_kernel(HeadBatch hb, float* __restrict__ part) {
-  constexpr int R = HB_WR, CPW = HB_CPW;
-  const int k = hb_find(hb.w0, hb.n, blockIdx.x);
+// filter gradient item: HB_CH channels x a run of T tiles: sum_p dy[p] x[src(p, tap)] per
+// (channel, tap) in lane registers, wave-summed once at the end of the run into partial row
+// `run`; the 4-channel chunk 0 also sums dy (the bias gradient) in fp64.
+template <int V>
+__device__ void heads_wgrad_body(const HeadBatch& hb, int k, long item, float* __restrict__ part) {
   const HeadJob& J = hb.j[k];
-  const int Rk = hb.WR[k];
-  const StripGeo g = hb_geo(J, Rk);
-  const long lb = blockIdx.x - hb.w0[k];
-  const int cblk = (int)(lb % hb.CB[k]);
-  const int unit = (int)(lb / hb.CB[k]);
-  const int lane = threadIdx.x & 63, wq = threadIdx.x >> 6;
-  int b, y0, xx;
-  strip_unit(g, unit, Rk, b, y0, xx);
-  int co[3];
-  bool cv[3];
-  strip_cols<true>(xx, g.W, co, cv);
-  const bool live = xx < g.W;
-  const long HW = (long)g.H * g.W;
-  float gr[R];
-  double gs = 0.0;   // bias gradient in fp64: a long cancelling sum
+  const int lane = threadIdx.x & 63;
+  const int nch = (J.Cin + HB_CH - 1) / HB_CH;
+  const int ch = (int)(item % nch);
+  const int run = (int)(item / nch);
+  const long tb = (long)run * hb.T[k], te = min(hb.ntile[k], tb + hb.T[k]);
+  const int Wv = J.W / V;
+  const long HW = (long)J.H * J.W;
+  const int c0 = ch * HB_CH;
+  float acc[HB_CH][9];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    gr[r] = (r < Rk && live && y0 + r < g.H) ? J.dy[(long)b * HW + (long)(y0 + r) * g.W + xx] : 0.f;
-    gs += (double)gr[r];
-  }
-  const int c0 = (cblk * 4 + wq) * CPW;
-  const float* xb = J.x.p + img_off(J.x, b);
-  float acc[CPW][9];
+  for (int c = 0; c < HB_CH; ++c)
 #pragma unroll
-  for (int i = 0; i < CPW; ++i)
+    for (int q = 0; q < 9; ++q) acc[c][q] = 0.f;
+  double gs = 0.0;
+  for (long t = tb; t < te; ++t) {
+    const HbPix p = hb_pix<V>(J, t, lane);
+    float g[V];
+    vload<V>(J.dy + (long)p.b * HW + (long)p.y * J.W + p.cx * V, g);
 #pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = 0.f;
+    for (int i = 0; i < V; ++i) g[i] = p.own ? g[i] : 0.f;    // halo lanes add nothing
+    if (ch == 0) {
 #pragma unroll
-  for (int i = 0; i < CPW; ++i) {
-    if (c0 + i < J.Cin) {
-      const float* xc = xb + (c0 + i) * HW;
-      float a0[3], a1[3], a2[3];
-      strip_row<true>(xc, y0 - 1, g.H, g.W, co, cv, a0);
-      strip_row<true>(xc, y0, g.H, g.W, co, cv, a1);
+      for (int i = 0; i < V; ++i) gs += (double)g[i];
+    }
+    const int ym = hb_reflect(p.y - 1, J.H), yp = hb_reflect(p.y + 1, J.H);
+    const float* xb = J.x.p + img_off(J.x, p.b);
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (r >= Rk) break;
-        strip_row<true>(xc, y0 + r + 1, g.H, g.W, co, cv, a2);
+    for (int c = 0; c < HB_CH; ++c) {
+      if (c0 + c >= J.Cin) break;
+      const float* xc = xb + (c0 + c) * HW;
+      float a0[V + 2], a1[V + 2], a2[V + 2];
+      hb_row_reflect<V>(xc, ym, J.W, p.cx, Wv, a0);
+      hb_row_reflect<V>(xc, p.y, J.W, p.cx, Wv, a1);
+      hb_row_reflect<V>(xc, yp, J.W, p.cx, Wv, a2);
+#pragma unroll
+      for (int i = 0; i < V; ++i)
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          acc[i][q] = fmaf(gr[r], a0[q], acc[i][q]);
-          acc[i][3 + q] = fmaf(gr[r], a1[q], acc[i][3 + q]);
-          acc[i][6 + q] = fmaf(gr[r], a2[q], acc[i][6 + q]);
+          acc[c][q] = fmaf(g[i], a0[i + q], acc[c][q]);
+          acc[c][3 + q] = fmaf(g[i], a1[i + q], acc[c][3 + q]);
+          acc[c][6 + q] = fmaf(g[i], a2[i + q], acc[c][6 + q]);
         }
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          a0[q] = a1[q];
-          a1[q] = a2[q];
-        }
-      }
     }
   }
-  const int ncol = J.Cin * 9 + 1;
-  float* dst = part + hb.p0[k] + (long)unit * ncol;
+  float* dst = part + hb.p0[k] + (long)run * J.Cin * 9;
 #pragma unroll
-  for (int i = 0; i < CPW; ++i)
+  for (int c = 0; c < HB_CH; ++c)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const float v = wave_sum(acc[i][t]);
-      if (lane == 0 && c0 + i < J.Cin) dst[(c0 + i) * 9 + t] = v;
+    for (int q = 0; q < 9; ++q) {
+      const float v = wave_sum_dpp(acc[c][q]);
+      if (lane == 0 && c0 + c < J.Cin) dst[(c0 + c) * 9 + q] = v;
     }
-  if (cblk == 0 && wq == 0) {   // bias: a long cancelling sum, kept in fp64 to the end
+  if (ch == 0) {
     const double v = wave_sum_d(gs);
-    if (lane == 0) reinterpret_cast<double*>(part)[hb.b0[k] + unit] = v;
+    if (lane == 0) reinterpret_cast<double*>(part)[hb.q0[k] + run] = v;
   }
 }
 
-// one block per column of every head (Cin*9 weights + the bias), fixed-order sum over its units
+// one launch, two wave ranges: [0, d0[n]) data-gradient items, then [d0[n], + w0[n]) filter-
+// gradient items (both read dy; only the data gradient writes, only the filter gradient reads x)
+__global__ __launch_bounds__(256) void heads_bwd_kernel(HeadBatch hb, float* __restrict__ part) {
+  long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w < hb.d0[hb.n]) {
+    const int k = hb_find(hb.d0, hb.n, w);
+    if (hb.V[k] == 4)
+      heads_dgrad_body<4>(hb, k, w - hb.d0[k]);
+    else
+      heads_dgrad_body<2>(hb, k, w - hb.d0[k]);
+    return;
+  }
+  w -= hb.d0[hb.n];
+  if (w >= hb.w0[hb.n]) return;                                // wave-uniform
+  const int k = hb_find(hb.w0, hb.n, w);
+  if (hb.V[k] == 4)
+    heads_wgrad_body<4>(hb, k, w - hb.w0[k], part);
+  else
+    heads_wgrad_body<2>(hb, k, w - hb.w0[k], part);
+}
+
+// one block per column of every head (Cin*9 weights + the bias), fixed-order sum over its runs
 __global__ __launch_bounds__(256) void heads_wgrad_reduce_kernel(HeadBatch hb, const float* __restrict__ part) {
   __shared__ float s_red[4];
+  __shared__ double s_dred[4];
   const int k = hb_find(hb.c0, hb.n, blockIdx.x);
   const HeadJob& J = hb.j[k];
   const int t = (int)(blockIdx.x - hb.c0[k]);
-  const int ncol = J.Cin * 9 + 1;
-  const StripGeo g = hb_geo(J, hb.WR[k]);
-  const long parts = (long)J.N * g.nband * g.nseg;
-  if (t == ncol - 1) {              // bias column: fp64 partials, fp64 sum
-    __shared__ double s_dred[4];
-    const double* bsrc = reinterpret_cast<const double*>(part) + hb.b0[k];
+  const int ncol = J.Cin * 9;
+  const long runs = hb.nrun[k];
+  if (t == ncol) {                  // bias column: fp64 partials, fp64 sum
+    const double* bsrc = reinterpret_cast<const double*>(part) + hb.q0[k];
     double d = 0.0;
-    for (long q = threadIdx.x; q < parts; q += 256) d += bsrc[q];
+    for (long q = threadIdx.x; q < runs; q += 256) d += bsrc[q];
     d = wave_sum_d(d);
     if ((threadIdx.x & 63) == 0) s_dred[threadIdx.x >> 6] = d;
     __syncthreads();
@@ -786,7 +892,7 @@ __global__ __launch_bounds__(256) void heads_wgrad_reduce_kernel(HeadBatch hb, c
   }
   const float* src = part + hb.p0[k] + t;
   float v = 0.f;
-  for (long q = threadIdx.x; q < parts; q += 256) v += src[q * ncol];
+  for (long q = threadIdx.x; q < runs; q += 256) v += src[q * ncol];
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -794,63 +900,67 @@ __global__ __launch_bounds__(256) void heads_wgrad_reduce_kernel(HeadBatch hb, c
   J.dw[t] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
 }
 
+// tiles per filter-gradient wave item: 8 (the 18 wave sums of a run amortised over 8 tiles x 2
+// channels), 1 on tiny heads
+int hb_tiles_per_item(long ntile) {
+  static const int T = tuning_knob("MD2_HEAD_T", 8);
+  return ntile >= 16L * T ? T : 1;
+}
+
 HeadBatch make_batch(const HeadJob* jobs, int n) {
   HeadBatch hb{};
   hb.n = n;
-  long u = 0, d = 0, w = 0, c = 0, p = 0;
+  long f = 0, d = 0, w = 0, c = 0, p = 0;
   for (int k = 0; k < n; ++k) {
     const HeadJob& j = jobs[k];
     hb.j[k] = j;
-    hb.u0[k] = u;
+    hb.V[k] = j.W % 4 == 0 ? 4 : 2;
+    const long nv = (long)j.N * j.H * (j.W / hb.V[k]);
+    hb.ntile[k] = cdiv(nv, HB_TILE);
+    hb.f0[k] = f;
+    f += hb.ntile[k];
+    hb.T[k] = hb_tiles_per_item(hb.ntile[k]);
+    hb.nrun[k] = cdiv(hb.ntile[k], hb.T[k]);
     hb.d0[k] = d;
+    d += hb.ntile[k] * cdiv(j.Cin, HB_DCH);
     hb.w0[k] = w;
+    w += (long)hb.nrun[k] * cdiv(j.Cin, HB_CH);
     hb.c0[k] = c;
-    hb.p0[k] = p;
-    // forward rows: 8 on the wide heads, fewer on the deep coarse ones (more units, shorter
-    // per-wave channel loops)
-    hb.FR[k] = j.H >= 64 ? HB_FR : (j.H >= 32 ? 4 : 2);
-    const long fu = (long)j.N * cdiv(j.H, hb.FR[k]) * cdiv(j.W, 64);
-    const long du = (long)j.N * cdiv(j.H, HB_DR) * cdiv(j.W, 64);
-    hb.WR[k] = j.H >= 64 ? HB_WR : 8;
-    const long wu = (long)j.N * cdiv(j.H, hb.WR[k]) * cdiv(j.W, 64);
-    // data-gradient channel groups: ~1024 wave units per head, >= 4 channels per group
-    hb.G[k] = (int)std::max<long>(1, std::min<long>(cdiv(1024, du), j.Cin / 4));
-    hb.CB[k] = cdiv(j.Cin, 4 * HB_CPW);
-    u += fu;
-    d += cdiv(du * hb.G[k], 4);
-    w += wu * hb.CB[k];
     c += (long)j.Cin * 9 + 1;
-    p += wu * ((long)j.Cin * 9 + 1);
+    hb.p0[k] = p;
+    p += (long)hb.nrun[k] * j.Cin * 9;
   }
-  hb.u0[n] = u;
+  hb.f0[n] = f;
   hb.d0[n] = d;
   hb.w0[n] = w;
   hb.c0[n] = c;
-  long bq = (p + 1) / 2;            // doubles start after the float rows (8-byte aligned)
+  long q = (p + 1) / 2;             // doubles start after the float rows (8-byte aligned)
   for (int k = 0; k < n; ++k) {
-    hb.b0[k] = bq;
-    bq += (long)jobs[k].N * cdiv(jobs[k].H, hb.WR[k]) * cdiv(jobs[k].W, 64);
+    hb.q0[k] = q;
+    q += hb.nrun[k];
   }
   return hb;
 }
 
 long heads_parts_floats(const HeadJob* jobs, int n) {
-  long f = 0, units = 0;
-  for (int k = 0; k < n; ++k) {
-    const long u = (long)jobs[k].N * cdiv(jobs[k].H, jobs[k].H >= 64 ? HB_WR : 8) * cdiv(jobs[k].W, 64);
-    f += u * (jobs[k].Cin * 9 + 1);
-    units += u;
-  }
-  return (f + 1) / 2 * 2 + 2 * units;   // float rows, then one fp64 bias partial per unit
+  const HeadBatch hb = make_batch(jobs, n);
+  long q = hb.q0[n - 1] + hb.nrun[n - 1];
+  return 2 * q;
 }
 
 int check_jobs(const HeadJob* jobs, int n) {
   MD2_CHECK_ARG(jobs && n >= 1 && n <= MAX_HEADS, "heads: 1..5 heads");
   for (int k = 0; k < n; ++k) {
     const HeadJob& j = jobs[k];
-    MD2_CHECK_ARG(j.Cin >= 1 && j.H >= 2 && j.W >= 2 && j.N >= 1 && j.x.p, "heads: shape / input");
+    MD2_CHECK_ARG(j.Cin >= 1 && j.H >= 2 && j.W >= 4 && j.W % 2 == 0 && j.N >= 1 && j.x.p,
+                  "heads: shape (W even, >= 4) / input");
     MD2_CHECK_ARG((long)j.N * j.H * j.W < (1L << 31) && (long)j.Cin * j.H * j.W < (1L << 31),
                   "heads: size");
+    const int V = j.W % 4 == 0 ? 4 : 2;
+    // vector loads / stores: every plane and image base V-float aligned
+    MD2_CHECK_ARG(j.x.bs0 % V == 0 && j.x.bhi % V == 0 && j.dxbs % V == 0 && j.ybs % V == 0 &&
+                      ((uintptr_t)j.x.p % (4 * V)) == 0,
+                  "heads: vector alignment");
   }
   return MD2_OK;
 }
@@ -980,7 +1090,7 @@ int heads_fwd(const HeadJob* jobs, int n, int act, hipStream_t st) {
   for (int k = 0; k < n; ++k) MD2_CHECK_ARG(jobs[k].y && jobs[k].wf.p, "heads_fwd: output / weights");
   HeadBatch hb = make_batch(jobs, n);
   hb.act = act;
-  hipLaunchKernelGGL(heads_fwd_kernel, dim3((unsigned)hb.u0[n]), dim3(256), 0, st, hb);
+  hipLaunchKernelGGL(heads_fwd_kernel, dim3((unsigned)hb.f0[n]), dim3(256), 0, st, hb);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
@@ -994,10 +1104,11 @@ int heads_bwd(const HeadJob* jobs, int n, void* ws, size_t ws_bytes, hipStream_t
   for (int k = 0; k < n; ++k)
     MD2_CHECK_ARG(jobs[k].dy && jobs[k].dx && jobs[k].dw && jobs[k].wd.p, "heads_bwd: pointers");
   MD2_CHECK_ARG(ws && ws_bytes >= heads_bwd_workspace(jobs, n), "heads_bwd workspace");
+  for (int k = 0; k < n; ++k)
+    MD2_CHECK_ARG(((uintptr_t)jobs[k].dx % 16) == 0 && ((uintptr_t)jobs[k].dy % 16) == 0, "heads_bwd: alignment");
   const HeadBatch hb = make_batch(jobs, n);
-  hipLaunchKernelGGL(heads_dgrad_kernel, dim3((unsigned)hb.d0[n]), dim3(256), 0, st, hb);
-  MD2_LAUNCH_CHECK();
-  hipLaunchKernelGGL(heads_wgrad_kernel, dim3((unsigned)hb.w0[n]), dim3(256), 0, st, hb, (float*)ws);
+  hipLaunchKernelGGL(heads_bwd_kernel, dim3((unsigned)cdiv(hb.d0[n] + hb.w0[n], 4)), dim3(256), 0, st, hb,
+                     (float*)ws);
   MD2_LAUNCH_CHECK();
   hipLaunchKernelGGL(heads_wgrad_reduce_kernel, dim3((unsigned)hb.c0[n]), dim3(256), 0, st, hb,
                      (const float*)ws);

@@ -564,7 +564,7 @@ class Model {
     if (h != cfg.H || w != cfg.W) {
       // the final branch must come back to full resolution for the loss (levels up to 5)
     }
-    if (batched_heads) {
+    {
       HeadJob jobs[MAX_HEADS];
       const int nh = head_jobs(jobs, ND);
       if (nh > 0) MD2_TRY(alloc(&hws, heads_bwd_workspace(jobs, nh) / sizeof(float) + 64));
@@ -950,12 +950,10 @@ class Model {
         }
       }
       MD2_TRY(conv_f(d.c2, nimg, in, d.o2, co * hw2, ACT_ELU, 0, st));
-      if (d.head >= 0 && !batched_heads)
-        MD2_TRY(conv_f(d.hc, nimg, tin(d.o2, co, hw2), d.disp, hw2, ACT_SIGMOID, 0, st));
       x = d.o2;
       C = co;
     }
-    if (batched_heads) {
+    {
       HeadJob jobs[MAX_HEADS];
       const int nh = head_jobs(jobs, nimg);
       hipEvent_t e = prof_begin(st);
@@ -965,9 +963,7 @@ class Model {
     return MD2_OK;
   }
 
-  // the DepthDecoder's disparity heads as one batch (head.h): MD2_HEADS_BATCH=0 runs them one
-  // conv at a time (A/B)
-  const bool batched_heads = tuning_knob("MD2_HEADS_BATCH", 1) != 0;
+  // the DepthDecoder's disparity heads run as one batch per pass (head.h)
   float* hws = nullptr;
   int head_jobs(HeadJob* jobs, int nimg) {
     int n = 0;
@@ -1329,7 +1325,7 @@ class Model {
     float* d_f4 = stages[3].back().d_out;
     // ---- DepthDecoder backward (reverse branch order), over ND decoder images
     const int nb = (int)br.size();
-    if (batched_heads) {
+    {
       // every head's data + filter gradient first (their d_head all come from the loss tail):
       // d_o2 of a head branch is then the head's dx, and the next branch's c1 dgrad adds to it
       HeadJob jobs[MAX_HEADS];
@@ -1354,9 +1350,6 @@ class Model {
       DecBranch& d = br[i];
       const long hw = (long)d.h * d.w, hw2 = 4 * hw;
       const int co = d.b.cout;
-      if (d.head >= 0 && !batched_heads) {
-        MD2_TRY(conv_wd(d.hc, ND, tin(d.o2, co, hw2), d.d_head, d.d_o2, co * hw2, i < nb - 1 ? 1 : 0, st));
-      }
       if (wov && i < nb - 1) MD2_HIP(hipStreamWaitEvent(st, ev_c2, 0));   // DPRE, bp_dec[0] free
       MD2_TRY(act_bias(d.o2, d.d_o2, DPRE, ND, co, hw2, ACT_ELU, st, wov ? bp_dec[0] : nullptr));
       TensorIn in = tin(d.up, co, hw2);
@@ -1409,7 +1402,7 @@ class Model {
         cin = br[i - 1].b.cout;
         xin = br[i - 1].o2;
         dx = br[i - 1].d_o2;
-        acc = (batched_heads && br[i - 1].head >= 0) ? 1 : 0;   // on top of the head's dx
+        acc = br[i - 1].head >= 0 ? 1 : 0;   // on top of the head's dx
       }
       if (wov) {
         MD2_TRY(wgrad_side(d.c1, tin(xin, cin, hw), DO1, ev_b, ev_c1));

@@ -35,21 +35,24 @@ def test_model_train_loss_parity(arch, sources):
     check_step(g, o, errs, b, label=f"R{arch} {sources}")
 
 
-@pytest.mark.parametrize("levels,target_id,source_ids", [((1, 3, 5), 1, (2, 3)), ((2, 4), 3, (1, 2)),
-                                                      ((1, 2, 3, 4, 5), 2, (3, 1))],
-                         ids=["levels135-target1", "levels24-target3", "levels12345-sources31"])
-def test_model_general_levels_and_frame_ids(levels, target_id, source_ids):
+@pytest.mark.parametrize("levels,target_id,source_ids,W", [((1, 3, 5), 1, (2, 3), 128), ((2, 4), 3, (1, 2), 128),
+                                                        ((1, 2, 3, 4, 5), 2, (3, 1), 128),
+                                                        ((1, 3, 5), 2, (1, 3), 96)],
+                         ids=["levels135-target1", "levels24-target3", "levels12345-sources31",
+                              "levels135-96wide"])
+def test_model_general_levels_and_frame_ids(levels, target_id, source_ids, W):
     """Any strictly increasing scale_levels in 1:5 (src/depth_decoder.jl:26-50, incl. the 1/16
     level 1 and a decoder that stops short of full resolution) and any target / two source frames
-    of the triplet (src/Monodepth.jl:49-60; pose pairs _get_pose_features, src/model.jl:64-69)."""
+    of the triplet (src/Monodepth.jl:49-60; pose pairs _get_pose_features, src/model.jl:64-69).
+    At width 96 the level-1 head is 6 pixels wide: its kernels move 2-pixel vectors."""
     from tests._model_parity import check_step, oracle_bounds, run
     kw = dict(levels=levels, target_id=target_id, source_ids=source_ids)
-    g, o, errs = run(sources="texture", **kw)
+    g, o, errs = run(sources="texture", W=W, **kw)
     assert len(g["disps"]) == len(levels)
     for l, d in zip(levels, g["disps"]):
-        assert d.shape[-2:] == (64 // 2 ** (5 - l), 128 // 2 ** (5 - l))
+        assert d.shape[-2:] == (64 // 2 ** (5 - l), W // 2 ** (5 - l))
     b = oracle_bounds(g, o, **kw)
-    check_step(g, o, errs, b, label=str(kw))
+    check_step(g, o, errs, b, label=f"{kw} W{W}")
 
 
 def test_backward_segments_cover_params():
