@@ -1267,32 +1267,51 @@ int concat_channels(const float* a, int ca, const float* b, int cb, int N, long 
   return MD2_OK;
 }
 
-// Tiled adjoint: a 32 x 8 block of input pixels of one plane stages the (2*8+4) x (2*32+4)
-// output-gradient window it reads in LDS (coalesced rows, each element fetched once instead of
-// up to 16 times through the cache), then every thread contracts its 6 x 6 window from LDS with
-// the same weights and the same summation order as upsample2_bwd_kernel (zero-weight terms add
-// +0, so the result is bit-identical).
-constexpr int UPB_TW = 32, UPB_TH = 8, UPB_FR = 2 * UPB_TH + 4, UPB_FC = 2 * UPB_TW + 4;
+// Tiled adjoint over the STACKED planes: the N*C input planes of h rows are one (N*C*h) x w
+// image, and input row r (plane r / h, local row r % h) reads output rows 2r-2 .. 2r+3 of the
+// equally stacked (N*C*2h) x 2w gradient, whatever plane they belong to -- an output row of a
+// neighbouring plane gets weight 0 from up_adj_weights (local index outside [0, 2h)), so a tile
+// may straddle planes and the small coarse levels (13 x 4 planes) fill whole blocks.  A block of
+// TW x TH input pixels stages its (2 TH + 4) x (2 TW + 4) output window in LDS with every
+// thread's loads issued before any LDS store (the one-at-a-time staging loop was latency-bound:
+// 39 us per launch), then contracts its 6 x 6 window from LDS with the same weights and the
+// same summation order as upsample2_bwd_kernel (bit-identical).
+template <int TW>
 __global__ __launch_bounds__(256) void upsample2_bwd_tile_kernel(const float* __restrict__ dy, int h,
-                                                                 int w, float ry, float rx,
+                                                                 int w, long rows, float ry, float rx,
                                                                  float* __restrict__ dx) {
-  __shared__ float t[UPB_FR][UPB_FC + 1];
-  const int W2 = 2 * w, H2 = 2 * h;
-  const int ix0 = blockIdx.x * UPB_TW, iy0 = blockIdx.y * UPB_TH;
-  const int oyb = 2 * iy0 - 2, oxb = 2 * ix0 - 2;
-  const float* g = dy + (long)blockIdx.z * H2 * W2;
-  for (int e = threadIdx.x; e < UPB_FR * UPB_FC; e += 256) {
-    const int r = e / UPB_FC, c = e - r * UPB_FC;
-    const int oy = oyb + r, ox = oxb + c;
-    t[r][c] = (oy >= 0 && oy < H2 && ox >= 0 && ox < W2) ? g[oy * W2 + ox] : 0.f;
+  constexpr int TH = 256 / TW, FR = 2 * TH + 4, FC = 2 * TW + 4;
+  constexpr int NL = (FR * FC + 255) / 256;
+  __shared__ float t[FR][FC + 1];
+  const int W2 = 2 * w;
+  const int ix0 = blockIdx.x * TW;
+  const long r0 = (long)blockIdx.y * TH;
+  const long oyb = 2 * r0 - 2, orows = 2 * rows;
+  const int oxb = 2 * ix0 - 2;
+  float v[NL];
+#pragma unroll
+  for (int q = 0; q < NL; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    const int r = e / FC, c = e - r * FC;
+    const long oy = oyb + r;
+    const int ox = oxb + c;
+    v[q] = (e < FR * FC && oy >= 0 && oy < orows && ox >= 0 && ox < W2) ? dy[oy * W2 + ox] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < NL; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    const int r = e / FC, c = e - r * FC;
+    if (e < FR * FC) t[r][c] = v[q];
   }
   __syncthreads();
-  const int tx = threadIdx.x % UPB_TW, ty = threadIdx.x / UPB_TW;
-  const int ix = ix0 + tx, iy = iy0 + ty;
-  if (ix >= w || iy >= h) return;
+  const int tx = threadIdx.x % TW, ty = threadIdx.x / TW;
+  const int ix = ix0 + tx;
+  const long row = r0 + ty;
+  if (ix >= w || row >= rows) return;
+  const int iy = (int)(row % h);
   int oy0, ox0;
   float wy[6], wx[6];
-  up_adj_weights(iy, ry, h, H2, oy0, wy);
+  up_adj_weights(iy, ry, h, 2 * h, oy0, wy);
   up_adj_weights(ix, rx, w, W2, ox0, wx);
   float s = 0.f;
 #pragma unroll
@@ -1302,7 +1321,7 @@ __global__ __launch_bounds__(256) void upsample2_bwd_tile_kernel(const float* __
     for (int b = 0; b < 6; ++b) acc += wx[b] * t[2 * ty + a][2 * tx + b];
     s += wy[a] * acc;
   }
-  dx[(long)blockIdx.z * h * w + iy * w + ix] = s;
+  dx[row * w + ix] = s;
 }
 
 static inline float up_ratio(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
@@ -1320,9 +1339,13 @@ int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStr
   const long n = (long)N * C * h * w;
   MD2_TRY(check_u31(4 * n));
   static const int tiled = tuning_knob("MD2_UP_TILED", 1);
-  if (tiled && (long)N * C <= 65535)
-    hipLaunchKernelGGL(upsample2_bwd_tile_kernel, dim3(cdiv(w, UPB_TW), cdiv(h, UPB_TH), N * C),
-                       dim3(256), 0, st, dy, h, w, up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx);
+  const long rows = (long)N * C * h;
+  if (tiled && w > 16 && cdiv(rows, 8) <= 65535)
+    hipLaunchKernelGGL(upsample2_bwd_tile_kernel<32>, dim3(cdiv(w, 32), cdiv(rows, 8)), dim3(256), 0, st, dy, h,
+                       w, rows, up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx);
+  else if (tiled && cdiv(rows, 16) <= 65535)
+    hipLaunchKernelGGL(upsample2_bwd_tile_kernel<16>, dim3(cdiv(w, 16), cdiv(rows, 16)), dim3(256), 0, st, dy, h,
+                       w, rows, up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx);
   else
     hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, h, w,
                        up_ratio(h, 2 * h), up_ratio(w, 2 * w), fd(w), fd(h), dx, (uint32_t)n);
@@ -1334,15 +1357,17 @@ int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStr
 // Pose head: Conv((1,1), 256=>6) + mean over (w,h) + 1e-2 scale (src/pose_decoder.jl:19,29-30).
 // mean(W x + b) = W mean(x) + b, so the 1x1 conv runs on the spatial means.
 // ---------------------------------------------------------------------------------------------
+// one wave per (pair, channel): lanes stride the plane, then a fixed-order wave sum (one thread
+// per channel walking its plane serially was latency-bound: 28 us for 24 x 256 planes of 52)
 __global__ __launch_bounds__(256) void pose_means_kernel(const float* __restrict__ x, int C, long HW,
                                                          float* __restrict__ means) {
-  const int q = blockIdx.x;
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const float* p = x + ((long)q * C + c) * HW;
-    float s = 0.f;
-    for (long i = 0; i < HW; ++i) s += p[i];
-    means[(long)q * C + c] = s / (float)HW;
-  }
+  const int q = blockIdx.x, c = blockIdx.y * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  const float* p = x + ((long)q * C + c) * HW;
+  float s = 0.f;
+  for (long i = lane; i < HW; i += 64) s += p[i];
+  s = wave_sum(s);
+  if (lane == 0) means[(long)q * C + c] = s / (float)HW;
 }
 
 __global__ __launch_bounds__(64) void pose_fc_kernel(const float* __restrict__ means, int C,
@@ -1358,7 +1383,7 @@ __global__ __launch_bounds__(64) void pose_fc_kernel(const float* __restrict__ m
 
 int pose_head_fwd(const float* x, int Q, int C, long HW, const float* w, const float* b,
                   float* means, float* pose, hipStream_t st) {
-  hipLaunchKernelGGL(pose_means_kernel, dim3(Q), dim3(256), 0, st, x, C, HW, means);
+  hipLaunchKernelGGL(pose_means_kernel, dim3(Q, cdiv(C, 4)), dim3(256), 0, st, x, C, HW, means);
   MD2_LAUNCH_CHECK();
   hipLaunchKernelGGL(pose_fc_kernel, dim3(Q, 6), dim3(64), 0, st, means, C, w, b, pose);
   MD2_LAUNCH_CHECK();
