@@ -36,7 +36,8 @@ def _model(seed=42, arch=18):
     import md2hip
     enc = md2hip.ResNet(arch, in_channels=3)
     return md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
-                                                 embedding_levels=0), md2hip.PoseDecoder(512), seed=seed)
+                                                 embedding_levels=0), md2hip.PoseDecoder(enc.stages[-1]),
+                        seed=seed)
 
 
 def _setup(model, N, h=H, w=W):
@@ -143,9 +144,20 @@ def test_world2_same_device_reduced_gradient_is_shard_sum(shape):
     procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, SHAPES[shape])) for r in range(2)]
     for p in procs:
         p.start()
+    import queue
+    import time
     res = {}
-    for _ in range(2):
-        r, local, reduced, flat = q.get(timeout=260)     # numpy: no fd sharing with the child
+    t0 = time.time()
+    while len(res) < 2:
+        try:
+            r, local, reduced, flat = q.get(timeout=5)   # numpy: no fd sharing with the child
+        except queue.Empty:
+            # a rank that died (exception, crash) never reports: fail now, not at the timeout
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"DP worker exited with {dead}"
+            assert time.time() - t0 < 260, "DP workers did not report"
+            print(f"waiting for DP workers ({time.time() - t0:.0f} s)", flush=True)
+            continue
         res[r] = (torch.from_numpy(local), torch.from_numpy(reduced), torch.from_numpy(flat))
     for p in procs:
         p.join(timeout=60)

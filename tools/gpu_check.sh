@@ -6,7 +6,7 @@
 TAG=${1:?tag}
 K=${2:-}
 mkdir -p gpurun_out
-ARGS=(tests -m gpu -v --timeout 600 --timeout-method thread -p no:cacheprovider)
+ARGS=(tests -m gpu -v -s --timeout 300 --timeout-method thread -p no:cacheprovider)
 [ -n "$K" ] && ARGS+=(-k "$K")
 timeout -k 10 1000 python -u -m pytest "${ARGS[@]}" > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?
