@@ -14,7 +14,36 @@
 
 #include <algorithm>
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <csignal>
+#include <unistd.h>
+
 namespace md2 {
+// MD2_SEGV_TRACE=1: on SIGSEGV / SIGABRT print the native backtrace (and this library's load base,
+// so `addr2line -e libmd2hip.so <pc - base>` maps the frames) before the default action -- host
+// debugging on a box where no debugger may attach to a GPU process.
+static void segv_trace(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  Dl_info di{};
+  if (dladdr((void*)&segv_trace, &di) && di.dli_fbase) {
+    char buf[96];
+    const int k = snprintf(buf, sizeof buf, "libmd2hip base %p\n", di.dli_fbase);
+    if (k > 0) (void)!write(2, buf, (size_t)k);
+  }
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+__attribute__((constructor)) static void install_segv_trace() {
+  const char* e = std::getenv("MD2_SEGV_TRACE");
+  if (e && std::atoi(e) == 1) {
+    signal(SIGSEGV, segv_trace);
+    signal(SIGABRT, segv_trace);
+  }
+}
+
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 const char* last_error() { return g_last_error.c_str(); }

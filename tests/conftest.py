@@ -3,6 +3,9 @@ import sys
 
 import pytest
 
+# a native crash in the library prints its backtrace (api.cpp; read when the library loads)
+os.environ.setdefault("MD2_SEGV_TRACE", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "monodepth2.jl_amd")
 for p in (ROOT, PKG):
