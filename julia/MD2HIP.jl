@@ -191,15 +191,38 @@ end
 (`cpu(disparities[end])` (W,H,1,n), `cpu.(warped_images)` two (W,H,C,n), `cpu(warp_loss)`
 (W,H,1,n); `nothing`s when `do_visualization` is false, :34-37,71-74).  The forward also runs the
 fused loss-tail pullback; the rrule finishes the backward.  `cache` / `params` are the ones the
-model was built with (md2_model_cfg); the arguments are kept for the reference's signature.
+model was built with (md2_model_cfg): any field that differs raises (`check_config`).
 
 Zygote: `gradient(() -> train_loss(m, x, ...)[1], Flux.params(m))` (the implicit-parameter loop
 of scripts/script.jl:84-86, src/simple_depth.jl:25-42) returns the gradient under `m.θ`, in
 m.θ's own layout, so `Flux.Optimise.update!(opt, Flux.params(m), ∇)` updates m.θ consistently.
 """
-train_loss(m::HIPModel, x::ROCArray{Float32,5}, auto_loss, cache, params,
-           do_visualization::Bool=false) =
+function train_loss(m::HIPModel, x::ROCArray{Float32,5}, auto_loss, cache, params,
+                    do_visualization::Bool=false)
+    check_config(m, cache, params)
     _train_loss(m, m.θ, x, auto_loss, do_visualization)     # m.θ read in traced code: accum_param
+end
+
+# The executor's kernels, buffers and loss-tail weights are built for ONE (Params, TrainCache)
+# (md2_model_cfg).  The reference reads them per call (src/training.jl:40-67), so a caller passing
+# a different cache / params must get an error, not the build-time config's loss.
+function check_config(m::HIPModel, cache, params)
+    c = m.cfg
+    bad = String[]
+    (params.batch_size, params.target_size...) == (c.batch, c.width, c.height) ||
+        push!(bad, "batch_size / target_size")
+    Float32(params.min_depth) == c.min_depth && Float32(params.max_depth) == c.max_depth ||
+        push!(bad, "min_depth / max_depth")
+    Float32(params.disparity_smoothness) == c.disparity_smoothness || push!(bad, "disparity_smoothness")
+    Cint(params.automasking) == c.automasking || push!(bad, "automasking")
+    (cache.target_id - 1, cache.source_ids[1] - 1, cache.source_ids[2] - 1) == (c.target, c.src0, c.src1) ||
+        push!(bad, "target_id / source_ids")
+    Float32.(cache.scales) == collect(c.scales[1:c.n_levels]) || push!(bad, "scales")
+    rowmajor(cache.K) == c.K && rowmajor(cache.invK) == c.invK || push!(bad, "K / invK")
+    isempty(bad) || error("train_loss: ", join(bad, ", "), " differ from the config the HIPModel was ",
+                          "built with (md2_model_cfg); build a HIPModel for this cache / params")
+    return nothing
+end
 
 function _train_loss(m::HIPModel, θ::ROCVector{Float32}, x::ROCArray{Float32,5}, auto_loss,
                      do_visualization::Bool)
@@ -582,7 +605,7 @@ end
 # (e.g. the job id) -- and the other ranks accept only a file carrying their own tag, so a file
 # left over from an earlier run can never hand them a stale id (ncclCommInitRank would hang).
 # ------------------------------------------------------------------------------------------------
-function comm_init(rank, nranks, device, idfile; run_id=get(ENV, "MD2_RUN_ID", ""))
+function comm_init(rank, nranks, device, idfile; run_id=get(ENV, "MD2_RUN_ID", ""), timeout_s=300)
     isempty(run_id) && error("comm_init: pass run_id (or set MD2_RUN_ID) unique to this launch")
     tag = Vector{UInt8}(run_id)
     id = zeros(UInt8, 128)
@@ -590,6 +613,7 @@ function comm_init(rank, nranks, device, idfile; run_id=get(ENV, "MD2_RUN_ID", "
         check(ccall((:md2_comm_get_unique_id, lib), Cint, (Ptr{UInt8},), id))
         write(idfile * ".tmp", vcat(id, tag)); mv(idfile * ".tmp", idfile; force=true)
     else
+        t0 = time()
         while true
             if isfile(idfile)
                 b = read(idfile)
@@ -598,6 +622,8 @@ function comm_init(rank, nranks, device, idfile; run_id=get(ENV, "MD2_RUN_ID", "
                     break
                 end
             end
+            time() - t0 > timeout_s && error("comm_init: rank ", rank, " saw no id file ", idfile,
+                                             " tagged ", run_id, " from rank 0 within ", timeout_s, " s")
             sleep(0.05)
         end
     end

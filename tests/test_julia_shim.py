@@ -168,7 +168,15 @@ def _function_body(jl, header_regex):
 def test_train_loss_return_convention(sources):
     jl, _ = sources
     # train_loss passes m.θ through traced code, so Zygote's implicit Params see the gradient
-    assert re.search(r"train_loss\(m::HIPModel[^)]*\)\s*=\s*\n?\s*_train_loss\(m, m\.θ,", jl)
+    tl = _function_body(jl, r"function train_loss\(m::HIPModel")
+    assert re.search(r"_train_loss\(m, m\.θ,", tl)
+    # the cache / params the caller passes must be the ones the executor was built for
+    assert "check_config(m, cache, params)" in tl
+    cc = _function_body(jl, r"function check_config\(m::HIPModel")
+    for field in ("batch_size", "target_size", "min_depth", "max_depth", "disparity_smoothness",
+                  "automasking", "target_id", "source_ids", "scales", "cache.K", "cache.invK"):
+        assert field in cc, field
+    assert "error(" in cc
     body = _function_body(jl, r"function _train_loss\(m::HIPModel")
     # the loss is a host scalar: copied out of the device vector before returning
     assert re.search(r"l = Array\(loss\)\[1\]", body)
@@ -198,3 +206,9 @@ def test_abi_version_pinned_in_every_binding():
     sys.path.insert(0, os.path.join(ROOT, "monodepth2.jl_amd"))
     from md2hip import _lib
     assert _lib.ABI_VERSION == v
+
+
+def test_comm_init_waits_with_a_timeout(sources):
+    jl, _ = sources
+    body = _function_body(jl, r"function comm_init\(")
+    assert "timeout_s" in body and re.search(r"time\(\) - t0 > timeout_s && error\(", body)
