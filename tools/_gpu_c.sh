@@ -1,4 +1,5 @@
 mkdir -p gpurun_out
+timeout -k 10 60 tools/micro/valu_rate > gpurun_out/valu_rate.txt 2>&1 || exit 2
 export MD2_SEGV_TRACE=1
 timeout -k 10 300 python -u tools/conv_accuracy.py gpurun_out/acc_px2.json > gpurun_out/acc_px2.log 2>&1 || exit 3
 MD2_TUNING=1 MD2_PX3=1 timeout -k 10 300 python -u tools/conv_accuracy.py gpurun_out/acc_px3.json > gpurun_out/acc_px3.log 2>&1 || exit 4
