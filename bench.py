@@ -184,13 +184,19 @@ def pmc_photo_traffic(batch):
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_photo.json")))
     if not files:
-        return None, None
+        return None, None, None
     with open(files[-1]) as f:
         d = json.load(f)
     row = d.get("by_batch", {}).get(str(batch))
     if not row or d.get("scales_per_launch") != 4:
-        return None, None
-    return row["traffic_bytes"], os.path.relpath(files[-1], ROOT)
+        return None, None, None
+    src = os.path.relpath(files[-1], ROOT)
+    # what bounds the kernel, from the same profile's counters (tools/pmc_photo_summary.py)
+    note = (f"{src} at B={batch}: {row['avg_us']:.1f} us/launch under the profiler, VALU issue "
+            f"utilisation {row['valu_issue_utilisation']:.2f}, waves active {row['active_inst_any']:.0%} / "
+            f"waiting {row['wait_any']:.0%}, {row['valu_insts_per_pixel_scale']:.0f} VALU instr per "
+            f"pixel-scale; traffic {row['traffic_bytes'] / row['algorithmic_bytes']:.2f}x algorithmic (DESIGN.md sec. 4)")
+    return row["traffic_bytes"], src, note
 
 
 def main():
@@ -325,12 +331,12 @@ def main():
                                "launches": n, "algorithmic_flop_per_step": flop, "kernel_ms_per_step": round(ms, 4)}
             ms, byt, n = prof["photometric"]
             gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-            ptraffic, psrc = pmc_photo_traffic(B) if (H, W) == (128, 416) else (None, None)
+            ptraffic, psrc, pnote = pmc_photo_traffic(B) if (H, W) == (128, 416) else (None, None, None)
             out["roofline_photometric"] = {"bound": "hbm", "kernel": "photo_stream_kernel (fused warp+SSIM+L1 fwd+bwd, all 4 scales in one launch)",
                                            "achieved": round(gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                            "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": ptraffic,
                                            "traffic_source": psrc,
-                                           "note": "issue-bound (waves 64% active at 2 waves/SIMD, 1141 VALU instr per pixel-scale), not HBM-bound: profiles/r03_pmc_photo.json, DESIGN.md sec. 4",
+                                           "note": pnote,
                                            "launches": n, "algorithmic_bytes_per_step": byt,
                                            "kernel_ms_per_step": round(ms, 4)}
             ms2, flop2, n2 = prof["conv_other"]
