@@ -16,7 +16,11 @@ struct ConvShape {
   int Cout, Ho, Wo; // output
   int KH, KW, stride, pad;
   int reflect;      // 1: NNlib pad_reflect(x, pad) + valid conv (src/depth_decoder.jl:5)
+  int cin_w;        // input channels of the WEIGHT tensor [Cout][cin_w][KH][KW] when the conv runs
+                    // on Cin > cin_w channels whose last Cin - cin_w are zero padding (their
+                    // packed weights are zero, their filter gradients are not produced); 0: Cin
 };
+inline int weight_cin(const ConvShape& s) { return s.cin_w > 0 ? s.cin_w : s.Cin; }
 
 // Input operand: channel concat of up to two tensors (cat(..., dims=3)), each [img][c][H][W].
 // p0 image offset = (b % bdiv) * bs0 + (b / bdiv) * bhi  (lets the stem read x[n][l] frames
@@ -88,6 +92,7 @@ struct PackJob {
   const float* w;
   PackDst f, d;        // forward (k over Cin, rows Cout) / dgrad (k over Cout, rows Cin)
   int Cout, Cin, KK;
+  int Cinw;            // the source weights' Cin (<= Cin: padded input channels stay zero)
   int tiled;           // both operands tap-major k-contiguous, Cin, Cout % 16 == 0: LDS tiles
   long block_begin;    // first block of this job in the batched grid
 };

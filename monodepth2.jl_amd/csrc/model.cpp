@@ -247,6 +247,10 @@ class Model {
   // h, w)) is the decoder's input / skip of level f; d_emb[f] its gradient, block-summed over the
   // planes into the target features' gradient (the _repeat pullback, src/repeat.jl:44-53).
   int E = 0, NP = 1, ND = 0;
+  // MPI mode: the E embedding channels of every decoder input are stored padded to Ep = E rounded
+  // up to 16 (zero channels with zero weights), so C + Ep stays a multiple of 16 and the decoder
+  // convs run on the tap-major kernels (conv_tap_major); the weights keep the reference's E
+  int Ep = 0;
   float* emb_in[5] = {};
   float* d_emb[5] = {};
   float* bins = nullptr;                        // [N][P]
@@ -391,10 +395,11 @@ class Model {
   float* P(long off) { return off >= 0 ? params + off : nullptr; }
   float* Gd(long off) { return off >= 0 ? grads + off : nullptr; }
 
-  int make_conv(RConv& r, const PConv& p, int H, int W, bool dgrad, size_t& ws_need) {
+  int make_conv(RConv& r, const PConv& p, int H, int W, bool dgrad, size_t& ws_need, int cin_pad = 0) {
     r.p = p;
     r.s.N = 0;
-    r.s.Cin = p.cin;
+    r.s.Cin = cin_pad > 0 ? cin_pad : p.cin;   // cin_pad: zero input channels beyond the weights' p.cin
+    r.s.cin_w = cin_pad > 0 ? p.cin : 0;
     r.s.Cout = p.cout;
     r.s.H = H;
     r.s.W = W;
@@ -439,6 +444,7 @@ class Model {
     B = 3 * N;
     E = A.emb;
     NP = E > 0 ? cfg.num_bins : 1;
+    Ep = E > 0 ? (E + 15) / 16 * 16 : 0;
     ND = N * NP;
     const int C = A.in_ch;
     size_t wsn = 0, wsn_side = 0, scratch = 0;   // wsn_side: side-stream convs (downsample, pose, decoder wgrad)
@@ -518,8 +524,8 @@ class Model {
     if (E > 0) {
       MD2_TRY(alloc(&bins, (long)N * NP));
       MD2_HIP(hipMemset(bins, 0, sizeof(float) * N * NP));
-      MD2_TRY(alloc(&emb_in[4], (long)ND * (featC[4] + E) * featH[4] * featW[4]));
-      MD2_TRY(alloc(&d_emb[4], (long)ND * (featC[4] + E) * featH[4] * featW[4]));
+      MD2_TRY(alloc(&emb_in[4], (long)ND * (featC[4] + Ep) * featH[4] * featW[4]));
+      MD2_TRY(alloc(&d_emb[4], (long)ND * (featC[4] + Ep) * featH[4] * featW[4]));
     }
     int h = featH[4], w = featW[4];
     for (auto& bs : spec.branches) {
@@ -527,9 +533,12 @@ class Model {
       d.b = bs;
       d.h = h;
       d.w = w;
-      MD2_TRY(make_conv(d.c1, bs.c1, h, w, true, wsn));
+      // MPI mode: the inputs carrying embedding channels run padded (Ep)
+      const int pad1 = (E > 0 && bs.bid == 1) ? bs.c1.cin - E + Ep : 0;
+      const int pad2 = (E > 0 && bs.cskip > 0) ? bs.c2.cin - E + Ep : 0;
+      MD2_TRY(make_conv(d.c1, bs.c1, h, w, true, wsn, pad1));
       need_ws(d.c1, ND, wsn, true);
-      MD2_TRY(make_conv(d.c2, bs.c2, 2 * h, 2 * w, true, wsn));
+      MD2_TRY(make_conv(d.c2, bs.c2, 2 * h, 2 * w, true, wsn, pad2));
       need_ws(d.c2, ND, wsn, true);
       need_ws(d.c1, ND, wsn_side, false);   // filter gradients on the side stream (wgrad_overlap)
       need_ws(d.c2, ND, wsn_side, false);
@@ -537,7 +546,7 @@ class Model {
       MD2_TRY(alloc(&d.up, (long)ND * bs.cout * 4 * h * w));
       MD2_TRY(alloc(&d.o2, (long)ND * bs.cout * 4 * h * w));
       MD2_TRY(alloc(&d.d_o2, (long)ND * bs.cout * 4 * h * w));
-      track((long)ND * (bs.cout + bs.cskip) * 4 * h * w);
+      track((long)ND * d.c2.s.Cin * 4 * h * w);
       if (bs.head >= 0) {
         d.head = bs.head;
         MD2_TRY(make_conv(d.hc, spec.heads[bs.head], 2 * h, 2 * w, true, wsn));
@@ -553,8 +562,8 @@ class Model {
         }
         MD2_TRY(alloc(&d_skip[fi], (long)N * featC[fi] * 4 * h * w));
         if (E > 0) {
-          MD2_TRY(alloc(&emb_in[fi], (long)ND * (featC[fi] + E) * 4 * h * w));
-          MD2_TRY(alloc(&d_emb[fi], (long)ND * (featC[fi] + E) * 4 * h * w));
+          MD2_TRY(alloc(&emb_in[fi], (long)ND * (featC[fi] + Ep) * 4 * h * w));
+          MD2_TRY(alloc(&d_emb[fi], (long)ND * (featC[fi] + Ep) * 4 * h * w));
         }
       }
       h *= 2;
@@ -723,7 +732,7 @@ class Model {
     recs.push_back(r);
   }
   static double conv_flops(const ConvShape& s) {
-    return 2.0 * s.N * (double)s.Ho * s.Wo * s.Cout * s.Cin * s.KH * s.KW;
+    return 2.0 * s.N * (double)s.Ho * s.Wo * s.Cout * weight_cin(s) * s.KH * s.KW;   // algorithmic
   }
 
   int conv_f(RConv& c, int nimg, const TensorIn& in, float* out, long out_bs, int act,
@@ -919,7 +928,8 @@ class Model {
       if (emb_in[fi]) {
         const long hw = (long)featH[fi] * featW[fi];
         MD2_TRY(mpi_embed_features(feat[fi] + (long)img0 * featC[fi] * hw, (long)featC[fi] * hw, nimg,
-                                   featC[fi], featH[fi], featW[fi], bins, NP, (E - 1) / 2, emb_in[fi], st));
+                                   featC[fi], featH[fi], featW[fi], bins, NP, (E - 1) / 2, emb_in[fi], st,
+                                   featC[fi] + Ep));
       }
     return MD2_OK;
   }
@@ -930,7 +940,7 @@ class Model {
     if (E > 0) {                       // decoder batch: nimg * P plane images
       MD2_TRY(mpi_embed(nimg, img0, st));
       x = emb_in[4];
-      C = featC[4] + E;
+      C = featC[4] + Ep;
       nimg *= NP;
     }
     for (auto& d : br) {
@@ -943,7 +953,7 @@ class Model {
         const int fi = 4 - d.b.bid;
         if (E > 0) {
           in.p1 = emb_in[fi];
-          in.bs1 = (long)(featC[fi] + E) * hw2;
+          in.bs1 = (long)(featC[fi] + Ep) * hw2;
         } else {
           in.p1 = feat[fi] + (long)img0 * featC[fi] * hw2;
           in.bs1 = (long)featC[fi] * hw2;
@@ -1359,9 +1369,9 @@ class Model {
         const int fi = 4 - d.b.bid;
         if (E > 0) {
           in.p1 = emb_in[fi];
-          in.bs1 = (long)(featC[fi] + E) * hw2;
+          in.bs1 = (long)(featC[fi] + Ep) * hw2;
           dskip = d_emb[fi];
-          skip_bs = (long)(featC[fi] + E) * hw2;
+          skip_bs = (long)(featC[fi] + Ep) * hw2;
         } else {
           in.p1 = feat[fi] + (long)T0 * featC[fi] * hw2;
           in.bs1 = (long)featC[fi] * hw2;
@@ -1378,7 +1388,7 @@ class Model {
       if (E > 0 && d.b.cskip > 0) {
         // _repeat pullback: the skip gradient of the target features = sum over the planes
         const int fi = 4 - d.b.bid;
-        MD2_TRY(plane_sum(d_emb[fi], N, NP, featC[fi] + E, featC[fi], hw2, d_skip[fi], 0, st));
+        MD2_TRY(plane_sum(d_emb[fi], N, NP, featC[fi] + Ep, featC[fi], hw2, d_skip[fi], 0, st));
       }
       if (wov && i < nb - 1) MD2_HIP(hipStreamWaitEvent(st, ev_c1, 0));   // DO1, bp_dec[1] free
       MD2_TRY(upsample2_bwd(DUP, ND, co, d.h, d.w, DO1, st));
@@ -1389,7 +1399,7 @@ class Model {
       int acc;
       if (i == 0 && ov) MD2_HIP(hipStreamWaitEvent(st, join_ev, 0));   // d_f4 written by the squeezer
       if (i == 0 && E > 0) {
-        cin = featC[4] + E;
+        cin = featC[4] + Ep;
         xin = emb_in[4];
         dx = d_emb[4];
         acc = 0;

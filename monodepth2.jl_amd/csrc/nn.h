@@ -105,8 +105,10 @@ int upsample2_fwd(const float* x, int N, int C, int h, int w, float* y, hipStrea
 int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStream_t st);
 // MPI-mode decoder input (src/model.jl:39-50): out[(b*P + p)][0:C] = feat[b], out[..][C + e] =
 // embed(bins[b][p])[e] broadcast over h x w (e < 2L+1: x, sin(2^i x), cos(2^i x))
+// Ctot: channels per output image (>= C + 2L + 1; the channels past C + 2L + 1 are written as
+// zeros -- the executor's padded layout); 0 = C + 2L + 1
 int mpi_embed_features(const float* feat, long sample_stride, int N, int C, int h, int w,
-                       const float* bins, int P, int L, float* out, hipStream_t st);
+                       const float* bins, int P, int L, float* out, hipStream_t st, int Ctot = 0);
 // the _repeat pullback (src/repeat.jl:44-53): out[b][c] (+)= sum_p in[b*P + p][c] for c < C of the
 // Cin channels per image (hw % 4 == 0)
 int plane_sum(const float* in, int N, int P, int Cin, int C, long hw, float* out, int accumulate,

@@ -1107,18 +1107,20 @@ __global__ __launch_bounds__(256) void upsample2_bwd_kernel(const float* __restr
 // output element; the embedding channel is recomputed per element (2 transcendental ops at most).
 __global__ __launch_bounds__(256) void mpi_embed_kernel(const float* __restrict__ feat, long sstride,
                                                         int C, int hw, const float* __restrict__ bins,
-                                                        int P, int E, float* __restrict__ out, long n) {
+                                                        int P, int E, int Ctot, float* __restrict__ out,
+                                                        long n) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const int CE = C + E;
   const int px = (int)(i % hw);
   const long t = i / hw;
-  const int c = (int)(t % CE);
-  const long img = t / CE;              // b * P + p
+  const int c = (int)(t % Ctot);
+  const long img = t / Ctot;            // b * P + p
   const int b = (int)(img / P), p = (int)(img - (long)b * P);
   float v;
   if (c < C) {
     v = feat[(long)b * sstride + (long)c * hw + px];
+  } else if (c >= C + E) {
+    v = 0.f;                            // zero padding channels (Ctot > C + E)
   } else {
     const int e = c - C;
     const float x = bins[(long)b * P + p];
@@ -1238,11 +1240,17 @@ int repeat_rows_adjoint(const float* src, long rows, int cols, int P, float* dst
 }
 
 int mpi_embed_features(const float* feat, long sample_stride, int N, int C, int h, int w,
-                       const float* bins, int P, int L, float* out, hipStream_t st) {
-  const long n = (long)N * P * (C + 2 * L + 1) * h * w;
+                       const float* bins, int P, int L, float* out, hipStream_t st, int Ctot) {
+  const int E = 2 * L + 1;
+  if (Ctot <= 0) Ctot = C + E;
+  if (Ctot < C + E) {
+    set_error("mpi_embed_features: output channels < C + 2L + 1");
+    return MD2_EINVAL;
+  }
+  const long n = (long)N * P * Ctot * h * w;
   MD2_TRY(check_u31(n));
   hipLaunchKernelGGL(mpi_embed_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, feat, sample_stride, C,
-                     h * w, bins, P, 2 * L + 1, out, n);
+                     h * w, bins, P, E, Ctot, out, n);
   MD2_LAUNCH_CHECK();
   return MD2_OK;
 }
