@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--width", type=int, default=416)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--layers", default="", help="write the per-layer conv table (markdown) here")
     args = ap.parse_args()
     import torch
     import md2hip
@@ -63,6 +64,30 @@ def main():
         p = ex.profile_read()
         prof = p if prof is None else {c: min(prof[c], p[c]) for c in p}
     ex.set_profiling(False)
+    if args.layers:
+        from collections import defaultdict
+        acc = defaultdict(lambda: [0.0, 0.0, 0])
+        for _ in range(3):
+            ex.set_profiling(True)
+            step()
+            torch.cuda.synchronize()
+            for t, cat, tms, work in ex.profile_records():
+                if cat == "photometric":
+                    continue
+                a = acc[t]
+                a[0] += tms / 3
+                a[1] = work
+                a[2] += 1
+            ex.set_profiling(False)
+        rows = sorted(acc.items(), key=lambda kv: -kv[1][0])
+        lines = [f"# MPI-mode per-layer conv table: {nb} planes, {W}x{H}, batch 1 (HIP events, mean of 3 steps)", "",
+                 "| layer pass | calls | GFLOP/call | ms/step | TFLOP/s | % fp32 MFMA peak |", "|---|---|---|---|---|---|"]
+        for t, (tms, work, n) in rows:
+            per = n / 3
+            tf = work * per / (tms * 1e-3) / 1e12 if tms > 0 else 0.0
+            lines.append(f"| `{t}` | {per:.0f} | {work / 1e9:.2f} | {tms:.3f} | {tf:.1f} | {100 * tf / PEAK:.1f} |")
+        with open(args.layers, "w") as f:
+            f.write("\n".join(lines) + "\n")
     out = {"workload": f"MPI train step resnet18, DepthDecoder(embedding_levels=21), batch 1, {nb} planes, "
                        f"{W}x{H}, 4 scales, ADAM",
            "ms_per_step": round(ms, 4), "samples_per_s": round(1e3 / ms, 2),
