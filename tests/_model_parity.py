@@ -240,12 +240,18 @@ def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_i
 # ResNet-50 at 640x192 (profiles/r04_parity.json), because those gradients are cancelling sums.
 # Measured worst ratios (r04): backward 1.61 x max(1e-4, floor_b), end to end 1.09 x
 # max(1e-3, floor, explained).
-CEIL_BWD, CEIL_BWD_FLOOR = 1e-4, 2.0
+# Named exception (backward): `coherent`, the move of the EXACT gradient under a +-1-ulp jitter of
+# the fp32 camera inputs (K, K^-1, poses).  Any fp32 pipeline rounds the per-(sample, source)
+# warp maps once, which perturbs every pixel's warp coherently; the decoder's low-resolution
+# branches and heads sum ~10^5-10^6 such pixel gradients with cancellation, so for ResNet-50 at
+# 640x192 their coherent sensitivity (1.6e-4, profiles/r04_parity_r50.json) exceeds the absolute
+# 1e-4.  The backward ceiling admits 1.25 x coherent for those tensors and nothing more.
+CEIL_BWD, CEIL_BWD_FLOOR, CEIL_BWD_COHERENT = 1e-4, 2.0, 1.25
 CEIL_E2E, CEIL_E2E_FLOOR = 1e-3, 1.25
 
 
 def _ceilings(b, floor, k):
-    return (max(CEIL_BWD, CEIL_BWD_FLOOR * b["floor_b"][k]),
+    return (max(CEIL_BWD, CEIL_BWD_FLOOR * b["floor_b"][k], CEIL_BWD_COHERENT * b["coherent"][k]),
             max(CEIL_E2E, CEIL_E2E_FLOOR * max(floor[k], b["explained"][k])))
 
 
@@ -263,7 +269,7 @@ def check_step(g, o, errs, b, label=""):
       * loss within max(1e-6, 4 x its fp32 floor); disparities / poses within max(1e-5, 4 x floor);
       * BACKWARD, per tensor: |gpu - sub| within max(4 x the backward's fp32 floor, 4 x its coherent
         warp-constant sensitivity, 2e-5) -- the GPU reproduces the exact gradient at its own
-        forward point -- and never above max(1e-4, 2 x floor_b);
+        forward point -- and never above max(1e-4, 2 x floor_b, 1.25 x coherent);
       * END TO END, per tensor: |gpu - oracle| within max(4 x the fp32 floor, 2 x what the
         forward's rounding explains, the backward bound + what the forward explains, 2e-5), and
         never above max(1e-3, 1.25 x max(floor, explained)).
@@ -282,7 +288,7 @@ def check_step(g, o, errs, b, label=""):
            "loss_rel_err": abs(g["loss"] - o["loss"]) / abs(o["loss"]), "loss_floor": floor["__loss"],
            "disp_rel_err": [D.rel_err(a, r) for a, r in zip(g["disps"], o["disps"])],
            "pose_rel_err": D.rel_err(g["pose"], o["pose"]),
-           "ceilings": {"backward": [CEIL_BWD, CEIL_BWD_FLOOR], "end_to_end": [CEIL_E2E, CEIL_E2E_FLOOR]},
+           "ceilings": {"backward": [CEIL_BWD, CEIL_BWD_FLOOR, CEIL_BWD_COHERENT], "end_to_end": [CEIL_E2E, CEIL_E2E_FLOOR]},
            "tensors": {k: {"bwd_err": b["bwd"][k], "bwd_bound": bb[k], "bwd_ceiling": _ceilings(b, floor, k)[0],
                            "e2e_err": errs[k], "e2e_bound": be[k], "e2e_ceiling": _ceilings(b, floor, k)[1],
                            "floor": floor[k], "floor_b": b["floor_b"][k], "explained": b["explained"][k],
