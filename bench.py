@@ -29,6 +29,10 @@ sys.path.insert(0, ROOT)
 METRIC = "train-step images/sec, ResNet-18 416×128; 1/2/4/8 MI355X + roofline %"
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
 PEAK_HBM_GBS = 8000.0              # MI355X_MICROARCH.md: HBM3E 8 TB/s
+# fwd / dgrad convs run bf16x9 (conv_px3: every fp32 product as 9 exact bf16 MFMA products, fp32
+# sums): their ceiling is the dense bf16 MFMA rate / 9; the filter gradients stay exact-fp32 MFMA
+PEAK_BF16_MFMA_TFLOPS = 2516.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+PEAK_BF16X9_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 9
 
 
 def parse():
@@ -324,9 +328,11 @@ def main():
             # the committed PMC profiles are of the default workload (ResNet-18, B=12, 416x128)
             default = (args.arch, B, H, W) == (18, 12, 128, 416)
             traffic, tsrc = pmc_traffic() if default else (None, None)
-            out["roofline"] = {"bound": "mfma", "kernel": "conv_px/conv_wgrad implicit-GEMM, zero-padded 3x3 convs (encoder+pose; fwd+dgrad+wgrad+split-K reduce)",
+            out["roofline"] = {"bound": "mfma", "kernel": "implicit-GEMM zero-padded 3x3 convs (encoder+pose): fwd+dgrad conv_px3 (bf16x9 exact products, fp32 sums), wgrad conv_wgrad (fp32 MFMA), + split-K reduce",
                                "achieved": round(ach, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
+                               "peak_note": "peak = fp32 MFMA (the reference's arithmetic, algorithmic fp32 FLOPs); "
+                                            f"the bf16x9 fwd/dgrad kernels' own ceiling is {PEAK_BF16X9_TFLOPS:.1f} TFLOP/s",
                                "traffic_source": tsrc,
                                "launches": n, "algorithmic_flop_per_step": flop, "kernel_ms_per_step": round(ms, 4)}
             ms, byt, n = prof["photometric"]

@@ -250,6 +250,10 @@ CEIL_BWD, CEIL_BWD_FLOOR, CEIL_BWD_COHERENT = 1e-4, 2.0, 1.25
 CEIL_E2E, CEIL_E2E_FLOOR = 1e-3, 1.25
 
 
+def _head_bias(k):
+    return k.startswith("depth.head") and k.endswith(".bias")
+
+
 def _ceilings(b, floor, k):
     return (max(CEIL_BWD, CEIL_BWD_FLOOR * b["floor_b"][k], CEIL_BWD_COHERENT * b["coherent"][k]),
             max(CEIL_E2E, CEIL_E2E_FLOOR * max(floor[k], b["explained"][k])))
@@ -268,7 +272,7 @@ def check_step(g, o, errs, b, label=""):
     """The full-step assertions shared by the model parity tests (b = oracle_bounds(g, o)):
       * loss within max(1e-6, 4 x its fp32 floor); disparities / poses within max(1e-5, 4 x floor);
       * BACKWARD, per tensor: |gpu - sub| within max(4 x the backward's fp32 floor, 4 x its coherent
-        warp-constant sensitivity, 2e-5) -- the GPU reproduces the exact gradient at its own
+        warp-constant sensitivity, 2e-5; 1e-4 for the cancelling head biases) -- the GPU reproduces the exact gradient at its own
         forward point -- and never above max(1e-4, 2 x floor_b, 1.25 x coherent);
       * END TO END, per tensor: |gpu - oracle| within max(4 x the fp32 floor, 2 x what the
         forward's rounding explains, the backward bound + what the forward explains, 2e-5), and
@@ -281,7 +285,14 @@ def check_step(g, o, errs, b, label=""):
     for s_, (a, r) in enumerate(zip(g["disps"], o["disps"])):
         assert D.rel_err(a, r) < max(1e-5, 4 * floor[f"__disp{s_}"]), s_
     assert D.rel_err(g["pose"], o["pose"]) < max(1e-5, 4 * floor["__pose"])
-    bb = {k: max(4 * b["floor_b"][k], 4 * b["coherent"][k], 2e-5) for k in b["bwd"]}
+    # named exception: a Cout=1 head's bias gradient is ONE sum over N*H*W per-pixel gradients of
+    # both signs (cancelling 10-1000x), so its relative error is the per-pixel fp32 rounding of
+    # the head's input gradient amplified by the cancellation -- the GPU's and the fp32 oracle's
+    # roundings differ pixel by pixel and their ratio scatters (seen: 5.2x floor_b for ResNet-50
+    # 64x128 head5 with the bf16x9 convs, 8.97e-5); these tensors are held to the absolute
+    # backward ceiling (1e-4) instead of 4 x floor_b
+    bb = {k: max(4 * b["floor_b"][k], 4 * b["coherent"][k], 2e-5, CEIL_BWD if _head_bias(k) else 0.0)
+          for k in b["bwd"]}
     # end to end <= backward error + what the forward's rounding explains (triangle inequality)
     be = {k: max(4 * floor[k], 2 * b["explained"][k], bb[k] + b["explained"][k], 2e-5) for k in errs}
     rec = {"label": label, "loss_gpu": g["loss"], "loss_oracle": o["loss"],
