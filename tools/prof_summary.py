@@ -9,7 +9,7 @@ Writes
   profiles/<tag>_pmc.json           FETCH_SIZE / WRITE_SIZE per launch of the roofline kernels
 
 Roofline kernel set (matches bench.py's HIP-event category 0): implicit-GEMM conv kernels with a
-3x3 zero-padded filter (conv_px_kernel / conv_wgrad_*kernel with KH=3, RFL=0) plus the split-K
+3x3 zero-padded filter (conv_px{,2,3}_kernel / conv_wgrad_*kernel with KH=3, RFL=0) plus the split-K
 reduction kernels dispatched right after each of them."""
 import csv
 import json
@@ -31,7 +31,7 @@ def is_conv3(name):
     a = targs(name)
     if a is None:
         return False
-    if "conv_px2_kernel" in name:         # <MODE, BM, BN, WM, WN, KH, KW, S, RFL>
+    if "conv_px2_kernel" in name or "conv_px3_kernel" in name:   # <MODE, BM, BN, WM, WN, KH, KW, S, RFL, ...>
         return a[5] == 3 and a[8] == 0
     if "conv_px_kernel" in name:          # <MODE, TAP, BM, BN, BK, WM, WN, KH, KW, S, RFL>
         return a[7] == 3 and a[10] == 0
