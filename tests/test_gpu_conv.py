@@ -2,6 +2,8 @@
 fp64 torch-CPU convolutions (the oracle's F.conv2d, cross-correlation semantics).
 
 Tolerance: relative Frobenius error 1e-5 (exact-fp32 MFMA accumulation over K <= 8k terms)."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -160,3 +162,52 @@ def test_act_backward(act):
     got = ops.act_backward(out.detach().float().cuda(), dout.float().cuda(), act)
     torch.cuda.synchronize()
     assert D.rel_err(got, pre.grad) < 1e-5
+
+
+_VARIANT_CHILD = r"""
+import sys, json
+root = sys.argv[1]
+sys.path[:0] = [root, root + "/monodepth2.jl_amd"]
+import torch, torch.nn.functional as F
+from md2hip import ops
+from oracle import md2_oracle as O
+from tests import _data as D
+out = {}
+for xs, cout, k, st, pd, rf in [((36, 64, 32, 104), 64, 3, 1, 1, False), ((36, 128, 16, 52), 256, 3, 2, 1, False),
+                                ((36, 512, 4, 13), 512, 3, 1, 1, False), ((12, 128, 32, 104), 64, 3, 1, 1, True),
+                                ((36, 128, 16, 52), 256, 1, 2, 0, False)]:
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(*xs, generator=g, dtype=torch.float64).float().double()
+    w = (torch.randn(cout, xs[1], k, k, generator=g, dtype=torch.float64) / (xs[1] * k * k) ** 0.5).float().double()
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    pre = F.conv2d(O.pad_reflect(xr, pd), wr, stride=st) if rf else F.conv2d(xr, wr, stride=st, padding=pd)
+    dy = torch.randn(pre.shape, generator=g, dtype=torch.float64).float().double()
+    pre.backward(dy)
+    xg, wg = x.float().cuda(), w.float().cuda()
+    y = ops.conv2d(xg, wg, None, stride=st, pad=pd, reflect=rf)
+    dx = ops.conv2d_dgrad(dy.float().cuda(), wg, xs, stride=st, pad=pd, reflect=rf)
+    dw, _ = ops.conv2d_wgrad(xg, dy.float().cuda(), tuple(w.shape), stride=st, pad=pd, reflect=rf, bias=False)
+    torch.cuda.synchronize()
+    out[str((xs, cout, k, st, rf))] = [D.rel_err(y, pre.detach()), D.rel_err(dx, xr.grad), D.rel_err(dw, wr.grad)]
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("env", [{"MD2_PX3": "0"}, {"MD2_PX3_TERMS": "6"}, {"MD2_WPX": "1"}],
+                         ids=["fp32-mfma", "bf16x6", "wgrad-kcontig"])
+def test_conv_kernel_variants(env):
+    """The selectable conv kernels (MD2_TUNING=1): the exact-fp32 MFMA fwd/dgrad (conv_px2), the
+    bf16x6 split-product kernel and the k-contiguous wgrad kernel, on the encoder / decoder shapes
+    that reach them, within 1e-5 of fp64 like the defaults (test_conv_fwd_bwd)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if not k.startswith("MD2_")}
+    e.update(MD2_TUNING="1", **env)
+    r = subprocess.run([sys.executable, "-c", _VARIANT_CHILD, root], env=e, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    errs = json.loads(r.stdout.strip().splitlines()[-1])
+    bad = {k: v for k, v in errs.items() if max(v) >= 1e-5}
+    assert not bad, bad
