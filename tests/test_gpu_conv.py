@@ -193,12 +193,12 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("env", [{"MD2_PX3": "0"}, {"MD2_PX3_TERMS": "6"}, {"MD2_WPX": "1"}],
-                         ids=["fp32-mfma", "bf16x6", "wgrad-kcontig"])
+@pytest.mark.parametrize("env", [{"MD2_PX3": "0"}, {"MD2_PX3_TERMS": "9"}],
+                         ids=["fp32-mfma", "bf16x9"])
 def test_conv_kernel_variants(env):
-    """The selectable conv kernels (MD2_TUNING=1): the exact-fp32 MFMA fwd/dgrad (conv_px2), the
-    bf16x6 split-product kernel and the k-contiguous wgrad kernel, on the encoder / decoder shapes
-    that reach them, within 1e-5 of fp64 like the defaults (test_conv_fwd_bwd)."""
+    """The selectable fwd / dgrad conv kernels (MD2_TUNING=1): the exact-fp32 MFMA kernel
+    (conv_px2) and the nine-product bf16x9 form of conv_px3, on encoder / decoder shapes, within
+    1e-5 of fp64 like the default bf16x6 (test_conv_fwd_bwd)."""
     import json
     import subprocess
     import sys
