@@ -358,7 +358,18 @@ int md2_adam(float* p, const float* g, float* adam_m, float* adam_v, long long n
  * multiplied by grad_scale first (1/world_size after a sum all-reduce); re-packs weights */
 int md2_model_adam(md2_model* m, float* adam_m, float* adam_v, float lr, float beta1,
                    float beta2, float eps, int step, float grad_scale, void* stream);
-/* forward_loss + every backward segment + ADAM (single-GPU step) */
+/* The update of ONE backward segment's parameters (the range model_backward_segment returned):
+ * ADAM as md2_model_adam over that range + the re-pack of its conv weights, enqueued on the
+ * executor's own update stream ordered after everything enqueued on `stream` so far -- called
+ * right after md2_model_backward_segment(segment) (a DP caller: on the stream its bucket's
+ * all-reduce ran on) it runs beside the remaining backward.  Every segment of a step takes the
+ * same `step`.  md2_model_adam_join makes `stream` wait for all pending segment updates
+ * (md2_model_forward_loss, eval_disparity, md2_model_adam and the parameter copies join first). */
+int md2_model_adam_segment(md2_model* m, int segment, float* adam_m, float* adam_v, float lr,
+                           float beta1, float beta2, float eps, int step, float grad_scale, void* stream);
+int md2_model_adam_join(md2_model* m, void* stream);
+/* forward_loss + every backward segment + ADAM (single-GPU step; each segment's update beside
+ * the remaining backward) */
 int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, float* adam_m,
                          float* adam_v, float lr, int step, float* loss, void* stream);
 /* md2_model_train_step as ONE captured hipGraph (forward, loss, every backward segment, ADAM,

@@ -453,14 +453,29 @@ int md2_model_adam(md2_model* m, float* adam_m, float* adam_v, float lr, float b
                     (hipStream_t)stream);
 }
 
+int md2_model_adam_segment(md2_model* m, int segment, float* adam_m, float* adam_v, float lr,
+                           float beta1, float beta2, float eps, int step, float grad_scale, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_adam_segment(m->impl, segment, adam_m, adam_v, lr, beta1, beta2, eps, step, grad_scale,
+                            (hipStream_t)stream);
+}
+
+int md2_model_adam_join(md2_model* m, void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_adam_join(m->impl, (hipStream_t)stream);
+}
+
 int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, float* adam_m,
                          float* adam_v, float lr, int step, float* loss, void* stream) {
-  MD2_CHECK_ARG(m, "model");
+  MD2_CHECK_ARG(m && adam_m && adam_v && step >= 1, "train_step args");
   hipStream_t st = (hipStream_t)stream;
   MD2_TRY(model_forward_loss(m->impl, x, auto_loss, loss, nullptr, st));
-  for (int k = 0; k < model_num_segments(m->impl); ++k)
+  // each segment's update runs beside the remaining backward (model_adam_segment)
+  for (int k = 0; k < model_num_segments(m->impl); ++k) {
     MD2_TRY(model_backward_segment(m->impl, k, nullptr, nullptr, st));
-  return model_adam(m->impl, adam_m, adam_v, lr, 0.9f, 0.999f, 1e-8f, step, 1.f, st);
+    MD2_TRY(model_adam_segment(m->impl, k, adam_m, adam_v, lr, 0.9f, 0.999f, 1e-8f, step, 1.f, st));
+  }
+  return model_adam_join(m->impl, st);
 }
 
 int md2_model_train_step_graph(md2_model* m, const float* x, const float* auto_loss, float* adam_m,

@@ -201,9 +201,35 @@ int md2_model_train_step_dp(md2_model* m, md2_comm* c, const float* x, const flo
   MD2_CHECK_ARG(m && x && adam_m && adam_v && step >= 1, "train_step_dp args");
   hipStream_t st = (hipStream_t)stream;
   MD2_TRY(model_forward_loss(m->impl, x, auto_loss, loss, nullptr, st));
-  MD2_TRY(md2_model_backward_allreduce(m, c, stream));
   const float scale = c ? 1.f / (float)c->nranks : 1.f;
-  return model_adam(m->impl, adam_m, adam_v, lr, beta1, beta2, eps, step, scale, st);
+  const int nseg = model_num_segments(m->impl);
+  if (!c) {
+    for (int k = 0; k < nseg; ++k) {
+      MD2_TRY(model_backward_segment(m->impl, k, nullptr, nullptr, st));
+      MD2_TRY(model_adam_segment(m->impl, k, adam_m, adam_v, lr, beta1, beta2, eps, step, scale, st));
+    }
+    return model_adam_join(m->impl, st);
+  }
+  while ((int)c->ready.size() < nseg) {
+    hipEvent_t e;
+    MD2_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->ready.push_back(e);
+  }
+  // per bucket: the segment's backward on st, its all-reduce on the comm stream, then its ADAM +
+  // re-pack on the executor's update stream ordered after that all-reduce (model_adam_segment)
+  float* g = model_grads(m->impl);
+  for (int k = 0; k < nseg; ++k) {
+    long off = 0, len = 0;
+    MD2_TRY(model_backward_segment(m->impl, k, &off, &len, st));
+    MD2_HIP(hipEventRecord(c->ready[k], st));
+    MD2_HIP(hipStreamWaitEvent(c->stream, c->ready[k], 0));
+    MD2_RCCL(c->r, c->r->all_reduce(g + off, g + off, (size_t)len, ncclFloat32, ncclSum, c->comm,
+                                    c->stream));
+    MD2_TRY(model_adam_segment(m->impl, k, adam_m, adam_v, lr, beta1, beta2, eps, step, scale, c->stream));
+  }
+  MD2_HIP(hipEventRecord(c->done, c->stream));
+  MD2_HIP(hipStreamWaitEvent(st, c->done, 0));
+  return model_adam_join(m->impl, st);
 }
 
 }  // extern "C"

@@ -66,6 +66,13 @@ int model_backward_segment(Model* m, int k, long* off, long* len, hipStream_t st
 int model_adam(Model* m, float* adam_m, float* adam_v, float lr, float b1, float b2, float eps,
                int step, float grad_scale, hipStream_t st);
 int model_repack(Model* m, hipStream_t st);   // after the parameters changed
+// ADAM over backward segment k's parameter range + the re-pack of its conv weights, enqueued on
+// the executor's update stream after everything enqueued on st so far (call it right after
+// model_backward_segment(k) -- and after the bucket's all-reduce in DP); model_adam_join makes st
+// wait for all of them (forward_loss, eval, model_adam and the parameter copies join first)
+int model_adam_segment(Model* m, int k, float* adam_m, float* adam_v, float lr, float b1, float b2,
+                       float eps, int step, float grad_scale, hipStream_t st);
+int model_adam_join(Model* m, hipStream_t st);
 // forward + loss + backward + ADAM(0.9, 0.999, 1e-8) replayed as one captured hipGraph
 int model_train_step_graph(Model* m, const float* x, const float* auto_loss, float* adam_m,
                            float* adam_v, float lr, int step, float* loss, hipStream_t st);

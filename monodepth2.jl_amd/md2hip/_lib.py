@@ -109,6 +109,9 @@ _SIGS = {
     "md2_model_num_segments": (C.c_int, [P]),
     "md2_model_backward_segment": (C.c_int, [P, C.c_int, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong), P]),
     "md2_model_adam": (C.c_int, [P, P, P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_float, P]),
+    "md2_model_adam_segment": (C.c_int, [P, C.c_int, P, P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
+                                         C.c_float, P]),
+    "md2_model_adam_join": (C.c_int, [P, P]),
     "md2_model_train_step": (C.c_int, [P, P, P, P, P, C.c_float, C.c_int, P, P]),
     "md2_model_train_step_graph": (C.c_int, [P, P, P, P, P, C.c_float, C.c_int, P, P]),
     "md2_model_set_params": (C.c_int, [P, P, P]),

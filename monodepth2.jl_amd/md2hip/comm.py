@@ -3,9 +3,11 @@
 One process per GPU.  Rank 0 creates the 128-byte RCCL id (``unique_id()``) and ships it to the
 other ranks by any channel (here: a torch.distributed *gloo* broadcast, i.e. host control plane
 only -- gradients never pass through torch); ``Comm(rank, nranks, id, device)`` joins.  A train step
-is ``train_step_dp``: forward_loss, then ``md2_model_backward_allreduce`` (each backward segment
-followed by the RCCL sum of its gradient bucket on the communicator's stream, overlapped with the
-rest of the backward), then ADAM with 1/nranks."""
+is ``train_step_dp`` (md2_model_train_step_dp): forward_loss, then per backward segment the RCCL
+sum of its gradient bucket on the communicator's stream and, ordered after that all-reduce, the
+bucket's ADAM (1/nranks) + weight re-pack on the executor's update stream -- both overlapped
+with the rest of the backward.  ``backward_allreduce`` is the all-reduce half
+alone (md2_model_backward_allreduce)."""
 from __future__ import annotations
 
 import ctypes as C

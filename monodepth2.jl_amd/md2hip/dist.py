@@ -71,17 +71,29 @@ class GradAllReduce:
     def grad_scale(self) -> float:
         return 1.0 / self.world
 
+    @property
+    def active(self) -> bool:
+        """Whether bucket_ready launches collectives (world > 1, or forced)."""
+        return self.world > 1 or self.force
+
 
 def train_step(executor, model, opt, x, comm: Optional[GradAllReduce] = None, loss=None):
     """forward_loss -> backward segments (each followed by its bucket all-reduce) -> ADAM with
     gradient scale 1/world.  Returns the device loss tensor (this rank's shard loss)."""
     comm = comm or GradAllReduce()
     out = executor.forward_loss(x, None, loss=loss)
+    if comm.active:
+        for k in range(executor.nseg):
+            off, ln = executor.backward_segment(k)
+            comm.bucket_ready(model.grad, off, ln)
+        comm.wait()
+        opt.update(model, grad_scale=comm.grad_scale)
+        return out
+    # no exchange: each segment's update runs beside the remaining backward (same arithmetic)
     for k in range(executor.nseg):
-        off, ln = executor.backward_segment(k)
-        comm.bucket_ready(model.grad, off, ln)
-    comm.wait()
-    opt.update(model, grad_scale=comm.grad_scale)
+        executor.backward_segment(k)
+        opt.update_segment(model, k)
+    opt.finish(model)
     return out
 
 

@@ -509,6 +509,30 @@ class ADAM:
         model.touch()
         ex.version = model.version
 
+    def update_segment(self, model: Model, k: int, grad_scale: float = 1.0):
+        """The update of backward segment k's parameters alone (md2_model_adam_segment), beside the
+        rest of the backward; segment 0 opens the step.  ``finish`` closes it."""
+        import torch
+        if self.m is None:
+            self.m = torch.zeros_like(model.flat)
+            self.v = torch.zeros_like(model.flat)
+        ex = model._last
+        if ex is None:
+            raise RuntimeError("ADAM.update_segment needs a preceding train_loss/gradient")
+        if k == 0:
+            self.t += 1
+        check(lib().md2_model_adam_segment(ex.handle, k, ptr(self.m), ptr(self.v), self.eta, self.beta[0],
+                                           self.beta[1], self.eps, self.t, grad_scale,
+                                           stream_of(model.device)), "md2_model_adam_segment")
+
+    def finish(self, model: Model):
+        """After every segment's update_segment: the stream waits for them (the model's weights
+        are current for the next forward)."""
+        ex = model._last
+        check(lib().md2_model_adam_join(ex.handle, stream_of(model.device)), "md2_model_adam_join")
+        model.touch()
+        ex.version = model.version
+
 
 def train_step(model: Model, x, auto_loss, cache: TrainCache, params: Params, opt: ADAM):
     """One ``gradient(θ) do train_loss(...)[1] end`` + ``update!`` on one GPU."""
