@@ -12,6 +12,7 @@ SyncBN) -- the one documented difference from a single-device run of the global 
 The same code runs with the gloo backend on CPU tensors (tests/test_dist.py)."""
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 
@@ -82,7 +83,7 @@ def train_step(executor, model, opt, x, comm: Optional[GradAllReduce] = None, lo
     gradient scale 1/world.  Returns the device loss tensor (this rank's shard loss)."""
     comm = comm or GradAllReduce()
     out = executor.forward_loss(x, None, loss=loss)
-    if comm.active:
+    if comm.active or os.environ.get("MD2_SEG_UPDATE") == "0":   # MD2_SEG_UPDATE=0: one update at the end (A/B)
         for k in range(executor.nseg):
             off, ln = executor.backward_segment(k)
             comm.bucket_ready(model.grad, off, ln)
