@@ -470,6 +470,11 @@ int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, f
   MD2_CHECK_ARG(m && adam_m && adam_v && step >= 1, "train_step args");
   hipStream_t st = (hipStream_t)stream;
   MD2_TRY(model_forward_loss(m->impl, x, auto_loss, loss, nullptr, st));
+  if (!model_segment_update_enabled()) {   // measured default: one update after the backward
+    for (int k = 0; k < model_num_segments(m->impl); ++k)
+      MD2_TRY(model_backward_segment(m->impl, k, nullptr, nullptr, st));
+    return model_adam(m->impl, adam_m, adam_v, lr, 0.9f, 0.999f, 1e-8f, step, 1.f, st);
+  }
   // each segment's update runs beside the remaining backward (model_adam_segment)
   for (int k = 0; k < model_num_segments(m->impl); ++k) {
     MD2_TRY(model_backward_segment(m->impl, k, nullptr, nullptr, st));

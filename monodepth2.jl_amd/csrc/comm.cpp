@@ -202,6 +202,10 @@ int md2_model_train_step_dp(md2_model* m, md2_comm* c, const float* x, const flo
   hipStream_t st = (hipStream_t)stream;
   MD2_TRY(model_forward_loss(m->impl, x, auto_loss, loss, nullptr, st));
   const float scale = c ? 1.f / (float)c->nranks : 1.f;
+  if (!model_segment_update_enabled()) {   // measured default: one update after the last bucket
+    MD2_TRY(md2_model_backward_allreduce(m, c, stream));
+    return model_adam(m->impl, adam_m, adam_v, lr, beta1, beta2, eps, step, scale, st);
+  }
   const int nseg = model_num_segments(m->impl);
   if (!c) {
     for (int k = 0; k < nseg; ++k) {

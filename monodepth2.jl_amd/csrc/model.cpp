@@ -1737,6 +1737,14 @@ int model_adam_join(Model* m, hipStream_t st) {
   return m->adam_join(st);
 }
 
+bool model_segment_update_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MD2_SEG_UPDATE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 int model_repack(Model* m, hipStream_t st) {
   MD2_CHECK_ARG(m, "model");
   return m->repack(st);

@@ -73,6 +73,9 @@ int model_repack(Model* m, hipStream_t st);   // after the parameters changed
 int model_adam_segment(Model* m, int k, float* adam_m, float* adam_v, float lr, float b1, float b2,
                        float eps, int step, float grad_scale, hipStream_t st);
 int model_adam_join(Model* m, hipStream_t st);
+// whether the train-step entry points use the per-segment update: MD2_SEG_UPDATE=1 (default off --
+// at N=1 the concurrent updates slowed the step by 2%, profiles/r04_seg_update_ab.txt)
+bool model_segment_update_enabled();
 // forward + loss + backward + ADAM(0.9, 0.999, 1e-8) replayed as one captured hipGraph
 int model_train_step_graph(Model* m, const float* x, const float* auto_loss, float* adam_m,
                            float* adam_v, float lr, int step, float* loss, hipStream_t st);

@@ -83,7 +83,9 @@ def train_step(executor, model, opt, x, comm: Optional[GradAllReduce] = None, lo
     gradient scale 1/world.  Returns the device loss tensor (this rank's shard loss)."""
     comm = comm or GradAllReduce()
     out = executor.forward_loss(x, None, loss=loss)
-    if comm.active or os.environ.get("MD2_SEG_UPDATE") == "0":   # MD2_SEG_UPDATE=0: one update at the end (A/B)
+    # one update after the last bucket unless MD2_SEG_UPDATE=1 (concurrent per-segment updates
+    # measured 2% slower at N=1, profiles/r04_seg_update_ab.txt)
+    if comm.active or os.environ.get("MD2_SEG_UPDATE") != "1":
         for k in range(executor.nseg):
             off, ln = executor.backward_segment(k)
             comm.bucket_ready(model.grad, off, ln)

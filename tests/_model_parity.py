@@ -140,7 +140,7 @@ def _ulp_jitter(t, gen):
 def _oracle_grad(g, dt, arch, levels, target_id, source_ids, at_gpu=False, jitter=None):
     """The oracle's flat gradient in dtype ``dt`` with every GPU decision imposed.  ``at_gpu``:
     the loss tail is evaluated AT THE GPU's forward outputs (its disparities and poses value-
-    substituted into the oracle's graph, d_o + (d_gpu - d_o).detach()), so the result is the
+    substituted into the oracle's graph, the disparities' sigmoid derivative taken at d_gpu too), so the result is the
     exact gradient of the function at the GPU's own forward point -- what the GPU backward must
     reproduce, free of the forward's rounding.  ``jitter`` (a seed, with at_gpu): K, invK and the
     GPU poses each moved by +-1 fp32 ulp -- a coherent perturbation of every pixel's warp of the
@@ -163,7 +163,13 @@ def _oracle_grad(g, dt, arch, levels, target_id, source_ids, at_gpu=False, jitte
     if gen is not None:
         K, invK = _ulp_jitter(K, gen), _ulp_jitter(invK, gen)
     if at_gpu:
-        d_o = [d + (gd.to(dt).view_as(d) - d).detach() for d, gd in zip(d_o, g["disps"])]
+        # value AND sigmoid derivative at the GPU's disparity: the GPU's pullback multiplies by
+        # d_gpu (1 - d_gpu) (loss_kernels.hip disp-grad kernel), so the head's sigmoid' is part of
+        # its forward point, not of its backward
+        def _at(d, gd):
+            gd = gd.to(dt).view_as(d)
+            return gd + (d - d.detach()) * (gd * (1 - gd) / (d * (1 - d))).detach()
+        d_o = [_at(d, gd) for d, gd in zip(d_o, g["disps"])]
         pg = g["pose"].to(dt)
         if gen is not None:
             pg = _ulp_jitter(pg, gen)

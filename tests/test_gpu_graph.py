@@ -45,3 +45,26 @@ def test_graph_step_bitwise_equals_eager(automasking):
     lg = md2hip.dist.train_step(ex_g, mg, og, xs[0], comm)
     torch.cuda.synchronize()
     assert torch.equal(le, lg) and torch.equal(me.flat, mg.flat)
+
+
+def test_segment_update_bitwise_equals_single_update(monkeypatch):
+    """MD2_SEG_UPDATE=1: ADAM + re-pack of each backward segment on the executor's update stream
+    beside the remaining backward (md2_model_adam_segment / md2_model_adam_join) equals the one
+    update after the backward bit for bit -- parameters, moments, losses -- over steps that each
+    read the previous step's re-packed weights."""
+    import md2hip.dist
+    xs = [D.triplets(2, 3, 64, 128, seed=s).float().cuda().contiguous() for s in (5, 6, 7)]
+    ma, cache, params, oa = _setup(False)
+    mb, _, _, ob = _setup(False)
+    ex_a = ma.executor(tuple(xs[0].shape), cache, params)
+    ex_b = mb.executor(tuple(xs[0].shape), cache, params)
+    comm = md2hip.dist.GradAllReduce(force=False)
+    for i, x in enumerate(xs):
+        monkeypatch.setenv("MD2_SEG_UPDATE", "0")
+        la = md2hip.dist.train_step(ex_a, ma, oa, x, comm).clone()
+        monkeypatch.setenv("MD2_SEG_UPDATE", "1")
+        lb = md2hip.dist.train_step(ex_b, mb, ob, x, comm).clone()
+        torch.cuda.synchronize()
+        assert torch.equal(la, lb), (i, la, lb)
+        assert torch.equal(ma.flat, mb.flat), i
+        assert torch.equal(oa.m, ob.m) and torch.equal(oa.v, ob.v), i
