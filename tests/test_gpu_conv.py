@@ -37,6 +37,11 @@ CASES = [
     ((2, 32, 9, 13), 16, 3, 2, 1, False, None, False),           # stride-2 dgrad, Cout 16
     ((2, 16, 7, 9), 32, 1, 2, 0, False, None, False),            # 1x1/2, 16 channels
     ((2, 64, 6, 10), 48, 3, 1, 1, True, "elu", True),            # reflect, CW 64, Cout 48
+    # bf16 split-product wgrad (conv_wgrad_px3: pixel pairs): a pair wrapping to the next row (odd
+    # Wo), an odd pixel count per image (fp32 tap kernel fallback), Cout 96 (ragged row tile)
+    ((2, 64, 6, 7), 96, 3, 1, 1, True, "elu", True),
+    ((3, 64, 5, 7), 64, 3, 1, 1, False, None, False),
+    ((2, 128, 9, 14), 64, 3, 2, 1, False, "relu", True),
     # the model-parity configuration (6 frames of 64x128): tiny deep maps
     ((6, 64, 16, 32), 64, 3, 1, 1, False, None, False),          # layer1
     ((6, 64, 16, 32), 128, 3, 2, 1, False, None, False),         # layer2.0.conv1
@@ -193,11 +198,12 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("env", [{"MD2_PX3": "0"}, {"MD2_PX3_TERMS": "9"}],
+@pytest.mark.parametrize("env", [{"MD2_PX3": "0", "MD2_WPX3": "0"}, {"MD2_PX3_TERMS": "9"}],
                          ids=["fp32-mfma", "bf16x9"])
 def test_conv_kernel_variants(env):
-    """The selectable fwd / dgrad conv kernels (MD2_TUNING=1): the exact-fp32 MFMA kernel
-    (conv_px2) and the nine-product bf16x9 form of conv_px3, on encoder / decoder shapes, within
+    """The selectable conv kernels (MD2_TUNING=1): the exact-fp32 MFMA kernels (conv_px2 for
+    fwd / dgrad, conv_wgrad_tap for wgrad) and the nine-product bf16x9 form of conv_px3 /
+    conv_wgrad_px3, on encoder / decoder shapes, within
     1e-5 of fp64 like the default bf16x6 (test_conv_fwd_bwd)."""
     import json
     import subprocess
