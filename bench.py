@@ -29,10 +29,11 @@ sys.path.insert(0, ROOT)
 METRIC = "train-step images/sec, ResNet-18 416×128; 1/2/4/8 MI355X + roofline %"
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
 PEAK_HBM_GBS = 8000.0              # MI355X_MICROARCH.md: HBM3E 8 TB/s
-# fwd / dgrad convs run bf16x9 (conv_px3: every fp32 product as 9 exact bf16 MFMA products, fp32
-# sums): their ceiling is the dense bf16 MFMA rate / 9; the filter gradients stay exact-fp32 MFMA
+# the 3x3 convs (fwd, dgrad, wgrad) run bf16x6 (conv_px3 / conv_wgrad_px3: every fp32 operand
+# split exactly into 3 bf16 terms, the 6 partial products down to 2^-16 on the bf16 MFMA, fp32
+# sums): their own ceiling is the dense bf16 MFMA rate / 6
 PEAK_BF16_MFMA_TFLOPS = 2516.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
-PEAK_BF16X9_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 9
+PEAK_BF16X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 
 
 def parse():
@@ -328,11 +329,11 @@ def main():
             # the committed PMC profiles are of the default workload (ResNet-18, B=12, 416x128)
             default = (args.arch, B, H, W) == (18, 12, 128, 416)
             traffic, tsrc = pmc_traffic() if default else (None, None)
-            out["roofline"] = {"bound": "mfma", "kernel": "implicit-GEMM zero-padded 3x3 convs (encoder+pose): fwd+dgrad conv_px3 (bf16x9 exact products, fp32 sums), wgrad conv_wgrad (fp32 MFMA), + split-K reduce",
+            out["roofline"] = {"bound": "mfma", "kernel": "implicit-GEMM zero-padded 3x3 convs (encoder+pose): fwd+dgrad conv_px3, wgrad conv_wgrad_px3 (bf16x6 split products, fp32 sums), + split-K / wgrad reduce",
                                "achieved": round(ach, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
                                "peak_note": "peak = fp32 MFMA (the reference's arithmetic, algorithmic fp32 FLOPs); "
-                                            f"the bf16x9 fwd/dgrad kernels' own ceiling is {PEAK_BF16X9_TFLOPS:.1f} TFLOP/s",
+                                            f"the bf16x6 kernels' own ceiling is {PEAK_BF16X6_TFLOPS:.1f} TFLOP/s",
                                "traffic_source": tsrc,
                                "launches": n, "algorithmic_flop_per_step": flop, "kernel_ms_per_step": round(ms, 4)}
             ms, byt, n = prof["photometric"]

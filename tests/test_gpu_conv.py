@@ -42,6 +42,10 @@ CASES = [
     ((2, 64, 6, 7), 96, 3, 1, 1, True, "elu", True),
     ((3, 64, 5, 7), 64, 3, 1, 1, False, None, False),
     ((2, 128, 9, 14), 64, 3, 2, 1, False, "relu", True),
+    # 4 pixels per lane (64-row tiles, 64 / 128-channel tap blocks): groups wrapping a row (odd Wo),
+    # reflect borders inside a group
+    ((2, 64, 4, 13), 64, 3, 1, 1, False, None, False),
+    ((2, 128, 4, 7), 64, 3, 1, 1, True, "elu", True),
     # the model-parity configuration (6 frames of 64x128): tiny deep maps
     ((6, 64, 16, 32), 64, 3, 1, 1, False, None, False),          # layer1
     ((6, 64, 16, 32), 128, 3, 2, 1, False, None, False),         # layer2.0.conv1

@@ -37,6 +37,8 @@ def is_conv3(name):
         return a[7] == 3 and a[10] == 0
     if "conv_wgrad_stem_kernel" in name:   # <CIN>: the 7x7/2 stem
         return False
+    if "conv_wgrad_px3_kernel" in name:    # <BM, BN, WM, WN, KH, KW, S, RFL, CW, NT>
+        return a[4] == 3 and a[7] == 0
     if "conv_wgrad16_kernel" in name:      # <MT, KH, KW, RFL>
         return a[1] == 3 and a[3] == 0
     if "conv_wgrad" in name:               # <BM, BN, BK, WM, WN, KH, KW, S, RFL[, CW]>
