@@ -31,7 +31,7 @@ names = ["pose+depth decoders", "layer4", "layer3", "layer2", "layer1", "stem"]
 
 enc = md2hip.ResNet(args.arch, in_channels=3)
 model = md2hip.Model(enc, md2hip.DepthDecoder(encoder_channels=enc.stages, scale_levels=[2, 3, 4, 5],
-                                              embedding_levels=0), md2hip.PoseDecoder(512), seed=42)
+                                              embedding_levels=0), md2hip.PoseDecoder(enc.stages[-1]), seed=42)
 K, invK = md2hip.depth10k_intrinsics(W, H)
 cache = md2hip.TrainCache(K=K, invK=invK)
 params = md2hip.Params(target_size=(W, H), batch_size=B, automasking=False)
