@@ -7,7 +7,7 @@ import re
 import sys
 
 FAMILIES = [
-    ("conv 3x3/1x1/7x7 implicit GEMM (fwd/dgrad/wgrad)", r"conv_(px|px2|px3|px16|wgrad|wgrad_tap|wgrad16|wgrad_stem)_kernel"),
+    ("conv 3x3/1x1/7x7 implicit GEMM (fwd/dgrad/wgrad)", r"conv_(px|px2|px3|px16|wgrad|wgrad_tap|wgrad16|wgrad_stem|wgrad_px3)_kernel"),
     ("split-K / wgrad reductions", r"(splitk_reduce|wgrad_reduce)"),
     ("BatchNorm (+ fused stem max pool)", r"bn_|maxpool"),
     ("disparity heads (Cout=1)", r"head_"),
