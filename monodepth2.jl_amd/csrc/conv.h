@@ -69,7 +69,7 @@ struct ConvWorkspace {
 bool conv_tap_major(const ConvShape& s, int mode);
 // forward (mode 0) / dgrad (mode 1) run the k-contiguous kernel with packed layout 1
 bool conv_px2_used(const ConvShape& s, int mode);
-bool conv_px3_used(const ConvShape& s, int mode);    // conv_px2 shapes on the bf16x9 kernel
+bool conv_px3_used(const ConvShape& s, int mode);    // conv_px2 shapes + 32-row stride-1 forwards on the bf16x6 kernel
 bool conv_px16_used(const ConvShape& s, int mode);   // M <= 16 (16x16x4 MFMA kernel)
 
 // packed operand sizes (elements) -- weights are repacked K-major with zero padding
