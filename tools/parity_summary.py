@@ -1,0 +1,38 @@
+"""Condense the check_step parity records of a -m gpu run (gpurun_out/parity/*.json, written by
+tests/_model_parity.py before it asserts) into one committed file: per record the loss / forward
+errors and the 8 tensors closest to their bounds, with the worst ratios to bound and ceiling.
+    python tools/parity_summary.py [PARITY_DIR] OUT.json [full-record label -> OUT_full.json]"""
+import glob
+import json
+import os
+import sys
+
+src = sys.argv[1] if len(sys.argv) > 2 else "gpurun_out/parity"
+out = sys.argv[2] if len(sys.argv) > 2 else sys.argv[1]
+recs = {}
+for f in sorted(glob.glob(os.path.join(src, "*.json"))):
+    d = json.load(open(f))
+    t = d.get("tensors")
+    if not t:                                   # non-check_step records (e.g. a trajectory) verbatim
+        recs[os.path.basename(f)] = d
+        continue
+    rb = {k: v["bwd_err"] / v["bwd_bound"] for k, v in t.items()}
+    rc = {k: v["bwd_err"] / v["bwd_ceiling"] for k, v in t.items()}
+    eb = {k: v["e2e_err"] / v["e2e_bound"] for k, v in t.items()}
+    ec = {k: v["e2e_err"] / v["e2e_ceiling"] for k, v in t.items()}
+    worst = sorted(t, key=lambda k: -max(rb[k], eb[k]))[:8]
+    recs[d["label"]] = {"loss_rel_err": d["loss_rel_err"], "pose_rel_err": d["pose_rel_err"],
+                        "disp_rel_err_max": max(d["disp_rel_err"]), "worst_bwd": d["worst_bwd"],
+                        "worst_e2e": d["worst_e2e"], "max_bwd_err": max(v["bwd_err"] for v in t.values()),
+                        "max_bwd_over_bound": max(rb.values()), "max_bwd_over_ceiling": max(rc.values()),
+                        "max_e2e_over_bound": max(eb.values()), "max_e2e_over_ceiling": max(ec.values()),
+                        "tensors_worst8": {k: t[k] for k in worst}, "n_tensors": len(t)}
+ok = all(r.get("max_bwd_over_ceiling", 0) < 1 and r.get("max_e2e_over_ceiling", 0) < 1 and
+         r.get("max_bwd_over_bound", 0) < 1 and r.get("max_e2e_over_bound", 0) < 1 for r in recs.values())
+json.dump({"source": "tests/_model_parity.py check_step records (gpurun_out/parity/*.json) of a -m gpu run on MI355X",
+           "ceilings": next((json.load(open(f)).get("ceilings") for f in glob.glob(os.path.join(src, "*.json"))
+                             if "ceilings" in json.load(open(f))), None),
+           "all_within_bound_and_ceiling": ok,
+           "note": "per record: the 8 tensors closest to their bounds; ratios < 1 pass",
+           "records": recs}, open(out, "w"), indent=1)
+print(out, "records", len(recs), "all within bound and ceiling:", ok)
