@@ -9,6 +9,12 @@ remaining backward) + Flux ADAM update.  Inputs are resident in HBM before timin
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+``--gpus N`` with N > 1 and no launcher around it (WORLD_SIZE unset) starts the N local ranks
+itself (torchrun-style, before anything touches the GPU) and exits with their status; it exits
+non-zero when fewer than N devices are visible or when WORLD_SIZE disagrees with --gpus -- it
+never runs fewer ranks than asked.  The JSON line carries the communicator's own rank count
+(md2_comm_rank) and the all-reduce calls / bytes per step it counted (md2_comm_stats).
+
 Rank 0 prints ONE JSON line.  ``value`` = images (training triplets) per second for the whole
 job; ``roofline`` is measured live with HIP events on the model's stream around every
 encoder 3x3 conv launch (fwd + dgrad + wgrad, the MFMA-bound kernels); ``roofline_photometric``
@@ -58,7 +64,89 @@ def parse():
                          "(md2_comm_*, gloo only as the host control plane) or torch.distributed nccl")
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel step (process group, all-reduce) even at N = 1")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="test hook (tests/test_bench_launcher.py): the ranks run only the gloo "
+                         "control plane (one all-reduce, no GPU) and rank 0 prints the JSON line")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _visible_devices(selftest: bool) -> int:
+    """GPUs this process can see, counted WITHOUT initialising HIP (torch.cuda.device_count does
+    not on this image), so the parent may still start the ranks.  The launcher self-test takes
+    MD2_BENCH_FAKE_DEVICES instead (CPU-only containers)."""
+    if selftest and "MD2_BENCH_FAKE_DEVICES" in os.environ:
+        return int(os.environ["MD2_BENCH_FAKE_DEVICES"])
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_local(args) -> int:
+    """Start args.gpus ranks of this script on this node (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT, as torch.distributed.run sets them) and wait for all of
+    them.  Rank 0 prints the JSON line on the inherited stdout.  A rank that fails ends the others
+    (their exact PIDs) and its exit status is returned."""
+    import subprocess
+    n = args.gpus
+    have = _visible_devices(args.launcher_selftest)
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}; refusing to run "
+              f"fewer ranks", file=sys.stderr, flush=True)
+        return 2
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    print(f"bench.py: started {n} ranks (pids {[p.pid for p in procs]}), master 127.0.0.1:{port}",
+          file=sys.stderr, flush=True)
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank pid {p.pid} exited with {code}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def _selftest_rank(json_fd) -> None:
+    """--launcher-selftest body of one rank: gloo process group, one all-reduce of a ones vector
+    (its sum is the number of ranks that took part), rank 0 prints the JSON line."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    t = torch.ones(4)
+    dist.all_reduce(t)
+    got = int(t[0].item())
+    pids = [None] * world
+    dist.all_gather_object(pids, os.getpid())
+    if dist.get_rank() == 0:
+        line = {"metric": METRIC, "selftest": True, "n_gpus": world,
+                "comm": {"nranks": dist.get_world_size(), "allreduce_ranks_seen": got,
+                         "rank_pids": pids}}
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
+    dist.destroy_process_group()
+    if got != world:
+        raise SystemExit(f"all-reduce saw {got} ranks, expected {world}")
 
 
 def synthetic_batch(batch, height, width, rank, device):
@@ -206,18 +294,35 @@ def pmc_photo_traffic(batch):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us: start the ranks here, before this process touches the GPU
+        sys.exit(launch_local(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing to guess",
+              file=sys.stderr)
+        sys.exit(2)
     # libraries print banners on fd 1 (RCCL's version block, gloo's peer count): keep stdout for
     # the ONE JSON line -- everything else goes to stderr until it is printed
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
+    if args.launcher_selftest:
+        _selftest_rank(json_fd)
+        return
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dp = world > 1 or args.force_dp
+    if local >= torch.cuda.device_count():
+        print(f"bench.py: rank {rank} wants device {local}, {torch.cuda.device_count()} visible",
+              file=sys.stderr)
+        sys.exit(2)
     if dp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
@@ -247,8 +352,12 @@ def main():
     x = synthetic_batch(B, H, W, rank, dev)
     ex = model.executor(tuple(x.shape), cache, params)
     loss_buf = torch.empty(1, dtype=torch.float32, device=dev)
+    comm = None
     if dp and args.comm == "md2":
         comm = md2hip.comm.Comm(rank, world, md2hip.comm.broadcast_id(rank), local)
+        crank, cranks = comm.query()
+        if (crank, cranks) != (rank, world):
+            raise SystemExit(f"RCCL communicator reports rank {crank} of {cranks}, expected {rank} of {world}")
 
         def step():
             md2hip.comm.train_step_dp(ex, model, opt, x, comm, loss=loss_buf)
@@ -274,12 +383,31 @@ def main():
     loss_first = loss_buf.item()
     for _ in range(max(args.warmup - 1, 0)):
         step()
+    def comm_counts():
+        if comm is None:
+            return 0, 0
+        if isinstance(comm, md2hip.comm.Comm):
+            return comm.stats()
+        return comm.calls, comm.bytes
+
     barrier()
+    c0 = comm_counts()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     barrier()
     elapsed = time.perf_counter() - t0
+    c1 = comm_counts()
+    if comm is None:
+        comm_info = None
+    elif isinstance(comm, md2hip.comm.Comm):
+        comm_info = {"transport": "md2_comm (RCCL, library-owned)", "nranks": comm.query()[1]}
+    else:
+        comm_info = {"transport": f"torch.distributed {comm.backend}", "nranks": comm.world}
+    if comm_info is not None:
+        comm_info["allreduce_calls_per_step"] = (c1[0] - c0[0]) / args.steps
+        comm_info["allreduce_bytes_per_step"] = (c1[1] - c0[1]) / args.steps
+        comm_info["grad_bytes"] = model.grad.numel() * model.grad.element_size()
     if dp:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.comm == "torch" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -292,12 +420,16 @@ def main():
         # its bracket open while the GPU idles) and the first profiled step also creates the
         # event pool; take each category's minimum over a few profiled steps
         ex.set_profiling(True)
+        samples = []
         for _ in range(args.probe_steps):
             step()
             torch.cuda.synchronize()
-            p = ex.profile_read()
-            prof = p if prof is None else {c: min(prof[c], p[c]) for c in p}
+            samples.append(ex.profile_read())
         ex.set_profiling(False)
+        import statistics
+        # per category: the median step (reported) and the fastest one (beside it)
+        prof = {c: statistics.median_low([s_[c] for s_ in samples]) for c in samples[0]}
+        prof_min = {c: min(s_[c] for s_ in samples) for c in samples[0]}
 
     if rank == 0:
         imgs = world * B * args.steps
@@ -313,6 +445,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
+            "arithmetic": "fp32 tensors and sums; the 3x3 convs contract on the bf16 MFMA with every fp32 "
+                          "operand split exactly into 3 bf16 terms and the 6 largest partial products "
+                          "(bf16x6, error vs fp64 below the fp32-MFMA kernel's; DESIGN.md sec. 4)",
             "data": f"synthetic: uniform [0,1) RGB {W}x{H} triplets keyed by global sample index; "
                     "Flux-default random init (seed 42)",
             "config": {"workload": f"train_step resnet{args.arch} depth+pose decoders, 4-scale photometric loss, ADAM",
@@ -320,12 +455,15 @@ def main():
                        "parallelism": f"dp{world}",
                        "allreduce": ("rccl md2_comm (bucketed, overlapped with backward)" if args.comm == "md2"
                                      else "rccl torch.distributed (bucketed, overlapped)") if dp else None},
+            "comm": comm_info,
             "loss": loss_val,
             "loss_first_step": loss_first,   # == tests/golden/bench_first_loss.json (fp64 oracle) at B=12 416x128
         }
         if prof:
             ms, flop, n = prof["conv3x3_encoder"]
             ach = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+            ms_min = prof_min["conv3x3_encoder"][0]
+            ach_min = flop / (ms_min * 1e-3) / 1e12 if ms_min > 0 else 0.0
             # the committed PMC profiles are of the default workload (ResNet-18, B=12, 416x128)
             default = (args.arch, B, H, W) == (18, 12, 128, 416)
             traffic, tsrc = pmc_traffic() if default else (None, None)
@@ -335,7 +473,9 @@ def main():
                                "peak_note": "peak = fp32 MFMA (the reference's arithmetic, algorithmic fp32 FLOPs); "
                                             f"the bf16x6 kernels' own ceiling is {PEAK_BF16X6_TFLOPS:.1f} TFLOP/s",
                                "traffic_source": tsrc,
-                               "launches": n, "algorithmic_flop_per_step": flop, "kernel_ms_per_step": round(ms, 4)}
+                               "launches": n, "algorithmic_flop_per_step": flop, "kernel_ms_per_step": round(ms, 4),
+                               "probe": f"median of {args.probe_steps} profiled steps; fastest step "
+                                        f"{ms_min:.4f} ms = frac {ach_min / PEAK_FP32_MFMA_TFLOPS:.4f}"}
             ms, byt, n = prof["photometric"]
             gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
             ptraffic, psrc, pnote = pmc_photo_traffic(B) if (H, W) == (128, 416) else (None, None, None)
@@ -345,7 +485,9 @@ def main():
                                            "traffic_source": psrc,
                                            "note": pnote,
                                            "launches": n, "algorithmic_bytes_per_step": byt,
-                                           "kernel_ms_per_step": round(ms, 4)}
+                                           "kernel_ms_per_step": round(ms, 4),
+                                           "probe": f"median of {args.probe_steps} profiled steps; fastest "
+                                                    f"{prof_min['photometric'][0]:.4f} ms"}
             ms2, flop2, n2 = prof["conv_other"]
             out["conv_other"] = {"ms_per_step": round(ms2, 4), "tflops": round(flop2 / max(ms2, 1e-9) / 1e9, 3),
                                  "launches": n2}

@@ -368,8 +368,9 @@ int md2_model_adam(md2_model* m, float* adam_m, float* adam_v, float lr, float b
 int md2_model_adam_segment(md2_model* m, int segment, float* adam_m, float* adam_v, float lr,
                            float beta1, float beta2, float eps, int step, float grad_scale, void* stream);
 int md2_model_adam_join(md2_model* m, void* stream);
-/* forward_loss + every backward segment + ADAM (single-GPU step; each segment's update beside
- * the remaining backward) */
+/* forward_loss + every backward segment + ADAM (single-GPU step).  By default ONE update runs
+ * after the last segment; MD2_SEG_UPDATE=1 opts into each segment's update beside the remaining
+ * backward (md2_model_adam_segment; measured 2% slower at N=1) */
 int md2_model_train_step(md2_model* m, const float* x, const float* auto_loss, float* adam_m,
                          float* adam_v, float lr, int step, float* loss, void* stream);
 /* md2_model_train_step as ONE captured hipGraph (forward, loss, every backward segment, ADAM,
@@ -389,14 +390,19 @@ int md2_model_train_step_graph(md2_model* m, const float* x, const float* auto_l
  * md2_model_backward_allreduce: every backward segment on `stream`, each followed by the RCCL
  * sum of its (final) gradient range on the communicator's own stream -- bucketed, overlapped with
  * the rest of the backward; `stream` waits for all buckets before returning.  comm == NULL:
- * plain backward.  md2_model_train_step_dp: forward_loss + that + ADAM with grad_scale 1/nranks.
+ * plain backward.  md2_model_train_step_dp: forward_loss + that + ADAM with grad_scale 1/nranks
+ * (one update after the last bucket by default; MD2_SEG_UPDATE=1: each bucket's ADAM + re-pack
+ * on the update stream right after its all-reduce).
  * ---------------------------------------------------------------------------------------- */
 #define MD2_COMM_ID_BYTES 128
 typedef struct md2_comm md2_comm;
 int md2_comm_get_unique_id(char* id);
 int md2_comm_init(int rank, int nranks, const char* id, int device, md2_comm** out);
 int md2_comm_destroy(md2_comm* comm);
+/* rank and size as the RCCL communicator reports them (ncclCommUserRank / ncclCommCount) */
 int md2_comm_rank(const md2_comm* comm, int* rank, int* nranks);
+/* all-reduces enqueued through this communicator and their payload bytes, cumulative */
+int md2_comm_stats(const md2_comm* comm, long long* calls, long long* bytes);
 /* in-place sum all-reduce of n floats, on `stream` (RCCL's ordering) */
 int md2_comm_allreduce_sum(md2_comm* comm, float* buf, long long n, void* stream);
 int md2_model_backward_allreduce(md2_model* m, md2_comm* comm, void* stream);

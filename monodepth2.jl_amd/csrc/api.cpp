@@ -23,7 +23,11 @@ namespace md2 {
 // MD2_SEGV_TRACE=1: on SIGSEGV / SIGABRT print the native backtrace (and this library's load base,
 // so `addr2line -e libmd2hip.so <pc - base>` maps the frames) before the default action -- host
 // debugging on a box where no debugger may attach to a GPU process.
-static void segv_trace(int sig) {
+// The handler is installed with sigaction and chains to whatever handler was there before
+// (pytest's faulthandler prints the Python traceback); backtrace() is called once at install time
+// so libgcc's unwinder is already loaded when a crash happens (its first call may allocate).
+static struct sigaction g_prev_segv, g_prev_abrt;
+static void segv_trace(int sig, siginfo_t* info, void* uctx) {
   void* frames[64];
   const int n = backtrace(frames, 64);
   Dl_info di{};
@@ -33,14 +37,32 @@ static void segv_trace(int sig) {
     if (k > 0) (void)!write(2, buf, (size_t)k);
   }
   backtrace_symbols_fd(frames, n, 2);
-  signal(sig, SIG_DFL);
+  const struct sigaction& prev = sig == SIGSEGV ? g_prev_segv : g_prev_abrt;
+  if ((prev.sa_flags & SA_SIGINFO) && prev.sa_sigaction) {
+    prev.sa_sigaction(sig, info, uctx);
+    return;
+  }
+  if (prev.sa_handler != SIG_DFL && prev.sa_handler != SIG_IGN && prev.sa_handler) {
+    prev.sa_handler(sig);
+    return;
+  }
+  struct sigaction dfl {};
+  dfl.sa_handler = SIG_DFL;
+  sigemptyset(&dfl.sa_mask);
+  sigaction(sig, &dfl, nullptr);
   raise(sig);
 }
 __attribute__((constructor)) static void install_segv_trace() {
   const char* e = std::getenv("MD2_SEGV_TRACE");
   if (e && std::atoi(e) == 1) {
-    signal(SIGSEGV, segv_trace);
-    signal(SIGABRT, segv_trace);
+    void* warm[4];
+    (void)backtrace(warm, 4);
+    struct sigaction sa {};
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_SIGINFO;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+    sigaction(SIGABRT, &sa, &g_prev_abrt);
   }
 }
 

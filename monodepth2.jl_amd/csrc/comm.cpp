@@ -32,6 +32,10 @@ struct Rccl {
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                              hipStream_t) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
+  // optional (the tests' recording stub exports only the five above): the communicator's own
+  // view of its size and rank, reported by md2_comm_rank
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*user_rank)(const ncclComm_t, int*) = nullptr;
 };
 
 int rccl(Rccl** out) {
@@ -61,6 +65,8 @@ int rccl(Rccl** out) {
       r.destroy = (decltype(r.destroy))dlsym(r.h, "ncclCommDestroy");
       r.all_reduce = (decltype(r.all_reduce))dlsym(r.h, "ncclAllReduce");
       r.error_string = (decltype(r.error_string))dlsym(r.h, "ncclGetErrorString");
+      r.comm_count = (decltype(r.comm_count))dlsym(r.h, "ncclCommCount");
+      r.user_rank = (decltype(r.user_rank))dlsym(r.h, "ncclCommUserRank");
     }
   }
   if (!r.h || !r.get_unique_id || !r.init_rank || !r.destroy || !r.all_reduce || !r.error_string) {
@@ -92,7 +98,17 @@ struct md2_comm {
   hipStream_t stream = nullptr;              // RCCL's stream (the buckets)
   std::vector<hipEvent_t> ready;             // per bucket: its gradient range is final
   hipEvent_t done = nullptr;                 // every bucket reduced
+  long long calls = 0, bytes = 0;            // all-reduces enqueued and their payload (md2_comm_stats)
 };
+
+namespace {
+// every all-reduce of the library goes through here (counted for md2_comm_stats)
+ncclResult_t comm_allreduce(md2_comm* c, float* buf, size_t n, hipStream_t st) {
+  ++c->calls;
+  c->bytes += (long long)n * (long long)sizeof(float);
+  return c->r->all_reduce(buf, buf, n, ncclFloat32, ncclSum, c->comm, st);
+}
+}  // namespace
 
 extern "C" {
 
@@ -156,15 +172,26 @@ int md2_comm_destroy(md2_comm* c) {
 
 int md2_comm_rank(const md2_comm* c, int* rank, int* nranks) {
   MD2_CHECK_ARG(c, "comm");
-  if (rank) *rank = c->rank;
-  if (nranks) *nranks = c->nranks;
+  int r = c->rank, n = c->nranks;
+  // RCCL's own answer where the loaded library exports it (what the bench reports as the
+  // communicator's size); the values given to md2_comm_init otherwise
+  if (c->r->user_rank) MD2_RCCL(c->r, c->r->user_rank(c->comm, &r));
+  if (c->r->comm_count) MD2_RCCL(c->r, c->r->comm_count(c->comm, &n));
+  if (rank) *rank = r;
+  if (nranks) *nranks = n;
+  return MD2_OK;
+}
+
+int md2_comm_stats(const md2_comm* c, long long* calls, long long* bytes) {
+  MD2_CHECK_ARG(c, "comm");
+  if (calls) *calls = c->calls;
+  if (bytes) *bytes = c->bytes;
   return MD2_OK;
 }
 
 int md2_comm_allreduce_sum(md2_comm* c, float* buf, long long n, void* stream) {
   MD2_CHECK_ARG(c && buf && n >= 0, "allreduce args");
-  MD2_RCCL(c->r, c->r->all_reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm,
-                                  (hipStream_t)stream));
+  MD2_RCCL(c->r, comm_allreduce(c, buf, (size_t)n, (hipStream_t)stream));
   return MD2_OK;
 }
 
@@ -187,8 +214,7 @@ int md2_model_backward_allreduce(md2_model* m, md2_comm* c, void* stream) {
     MD2_TRY(model_backward_segment(m->impl, k, &off, &len, st));
     MD2_HIP(hipEventRecord(c->ready[k], st));
     MD2_HIP(hipStreamWaitEvent(c->stream, c->ready[k], 0));
-    MD2_RCCL(c->r, c->r->all_reduce(g + off, g + off, (size_t)len, ncclFloat32, ncclSum, c->comm,
-                                    c->stream));
+    MD2_RCCL(c->r, comm_allreduce(c, g + off, (size_t)len, c->stream));
   }
   MD2_HIP(hipEventRecord(c->done, c->stream));
   MD2_HIP(hipStreamWaitEvent(st, c->done, 0));
@@ -227,8 +253,7 @@ int md2_model_train_step_dp(md2_model* m, md2_comm* c, const float* x, const flo
     MD2_TRY(model_backward_segment(m->impl, k, &off, &len, st));
     MD2_HIP(hipEventRecord(c->ready[k], st));
     MD2_HIP(hipStreamWaitEvent(c->stream, c->ready[k], 0));
-    MD2_RCCL(c->r, c->r->all_reduce(g + off, g + off, (size_t)len, ncclFloat32, ncclSum, c->comm,
-                                    c->stream));
+    MD2_RCCL(c->r, comm_allreduce(c, g + off, (size_t)len, c->stream));
     MD2_TRY(model_adam_segment(m->impl, k, adam_m, adam_v, lr, beta1, beta2, eps, step, scale, c->stream));
   }
   MD2_HIP(hipEventRecord(c->done, c->stream));

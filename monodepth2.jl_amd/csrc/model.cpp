@@ -298,7 +298,7 @@ class Model {
   // updates (model_adam_join).
   hipStream_t upd = nullptr;
   hipEvent_t seg_ev = nullptr, upd_ev = nullptr;
-  bool upd_pending = false;
+  bool upd_recorded = false;   // upd_ev holds the newest adam_segment's completion
   struct SegPack {
     PackJob* jobs = nullptr;
     int njobs = 0;
@@ -908,13 +908,15 @@ class Model {
                       gscale, upd));
     if (seg_pack[k].njobs) MD2_TRY(conv_pack_batch(seg_pack[k].jobs, seg_pack[k].njobs, seg_pack[k].blocks, upd));
     MD2_HIP(hipEventRecord(upd_ev, upd));
-    upd_pending = true;
+    upd_recorded = true;
     return MD2_OK;
   }
-  // st waits for every update enqueued by adam_segment
+  // st waits for every update enqueued by adam_segment.  The ordering is per stream, so once an
+  // update was ever recorded EVERY join waits (an entry point on another stream -- a Python
+  // executor sharing the parameters, a user stream for eval or get_params -- must see it too);
+  // waiting on a completed event costs next to nothing.
   int adam_join(hipStream_t st) {
-    if (upd_pending) MD2_HIP(hipStreamWaitEvent(st, upd_ev, 0));
-    upd_pending = false;
+    if (upd_recorded) MD2_HIP(hipStreamWaitEvent(st, upd_ev, 0));
     return MD2_OK;
   }
 
@@ -1675,6 +1677,9 @@ int model_train_step_graph(Model* m, const float* x, const float* auto_loss, flo
     for (int k = 0; k < model_num_segments(m); ++k) MD2_TRY(model_backward_segment(m, k, nullptr, nullptr, st));
     return model_adam(m, adam_m, adam_v, lr, 0.9f, 0.999f, 1e-8f, step, 1.f, st);
   }
+  // the replay reads and writes params, adam_m / adam_v and the packed weights: order it after
+  // pending per-segment updates (outside the capture: the event lives outside the graph)
+  MD2_TRY(m->adam_join(st));
   if (!g.exec || g.adam_m != adam_m || g.adam_v != adam_v || g.lr != lr || g.with_auto != (int)with_auto)
     MD2_TRY(capture_step(m, with_auto, adam_m, adam_v, lr));
   const size_t xb = sizeof(float) * (size_t)m->N * 3 * m->cfg.arch.in_ch * m->cfg.H * m->cfg.W;
@@ -1747,6 +1752,7 @@ bool model_segment_update_enabled() {
 
 int model_repack(Model* m, hipStream_t st) {
   MD2_CHECK_ARG(m, "model");
+  MD2_TRY(m->adam_join(st));   // pending per-segment updates write the same packed weights
   return m->repack(st);
 }
 
@@ -1897,6 +1903,7 @@ int model_get_params_flux(Model* m, float* flux, hipStream_t st) {
 
 int model_get_grads_flux(Model* m, float* flux, hipStream_t st) {
   MD2_CHECK_ARG(m, "model");
+  MD2_TRY(m->adam_join(st));   // a DP per-segment update is ordered after its bucket's all-reduce
   return flux_flip_copy(m, m->grads, flux, st);
 }
 

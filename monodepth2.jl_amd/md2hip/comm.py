@@ -4,9 +4,10 @@ One process per GPU.  Rank 0 creates the 128-byte RCCL id (``unique_id()``) and 
 other ranks by any channel (here: a torch.distributed *gloo* broadcast, i.e. host control plane
 only -- gradients never pass through torch); ``Comm(rank, nranks, id, device)`` joins.  A train step
 is ``train_step_dp`` (md2_model_train_step_dp): forward_loss, then per backward segment the RCCL
-sum of its gradient bucket on the communicator's stream and, ordered after that all-reduce, the
-bucket's ADAM (1/nranks) + weight re-pack on the executor's update stream -- both overlapped
-with the rest of the backward.  ``backward_allreduce`` is the all-reduce half
+sum of its gradient bucket on the communicator's stream, overlapped with the rest of the backward
+(SURVEY.md 8(e)), then ONE ADAM (1/nranks) + weight re-pack after the last bucket.  With
+MD2_SEG_UPDATE=1 each bucket's ADAM + re-pack instead runs on the executor's update stream right
+after its all-reduce (opt-in: measured 2% slower at N=1).  ``backward_allreduce`` is the all-reduce half
 alone (md2_model_backward_allreduce)."""
 from __future__ import annotations
 
@@ -21,6 +22,7 @@ declare("md2_comm_get_unique_id", C.c_int, [C.c_char_p])
 declare("md2_comm_init", C.c_int, [C.c_int, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_void_p)])
 declare("md2_comm_destroy", C.c_int, [P])
 declare("md2_comm_rank", C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)])
+declare("md2_comm_stats", C.c_int, [P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)])
 declare("md2_comm_allreduce_sum", C.c_int, [P, P, C.c_longlong, P])
 declare("md2_model_backward_allreduce", C.c_int, [P, P, P])
 declare("md2_model_train_step_dp", C.c_int, [P, P, P, P, P, P, C.c_float, C.c_float, C.c_float, C.c_float,
@@ -62,6 +64,18 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+    def query(self):
+        """(rank, nranks) as the RCCL communicator itself reports them (md2_comm_rank)."""
+        r, n = C.c_int(), C.c_int()
+        check(lib().md2_comm_rank(self.handle, C.byref(r), C.byref(n)), "md2_comm_rank")
+        return r.value, n.value
+
+    def stats(self):
+        """(all-reduce calls, payload bytes) enqueued through this communicator so far."""
+        calls, nbytes = C.c_longlong(), C.c_longlong()
+        check(lib().md2_comm_stats(self.handle, C.byref(calls), C.byref(nbytes)), "md2_comm_stats")
+        return calls.value, nbytes.value
 
     def allreduce_sum(self, t):
         """In-place sum over ranks of a float32 CUDA tensor, ordered on the current stream."""

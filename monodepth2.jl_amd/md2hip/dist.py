@@ -47,6 +47,8 @@ class GradAllReduce:
         self.backend = dist.get_backend(group) if on else None
         self.force = force and on           # run the collective even at world size 1 (tests)
         self._handles: List = []
+        self.calls = 0                      # collectives launched and their payload (bench.py)
+        self.bytes = 0
 
     def bucket_ready(self, flat_grad, off: int, length: int):
         """Launch the sum all-reduce of flat_grad[off:off+length] (returns immediately)."""
@@ -54,6 +56,8 @@ class GradAllReduce:
             return
         import torch.distributed as dist
         sl = flat_grad[off:off + length]
+        self.calls += 1
+        self.bytes += length * sl.element_size()
         if self.backend == "gloo" and sl.is_cuda:
             # host control-plane backend (CPU tests, same-device rehearsal): stage through the host
             h = sl.cpu()

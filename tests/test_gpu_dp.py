@@ -243,3 +243,70 @@ def test_library_bucket_allreduce_order_with_recording_stub(shape):
     r = subprocess.run([sys.executable, "-c", _STUB_CHILD, root, shape], env=env, capture_output=True,
                        text=True, timeout=170)
     assert r.returncode == 0 and "STUB_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+_SEG_CHILD = r"""
+import ctypes as C, os, sys
+root, out = sys.argv[1], sys.argv[2]
+sys.path[:0] = [root, os.path.join(root, "monodepth2.jl_amd")]
+import numpy as np, torch, md2hip
+from md2hip import comm as MC
+from md2hip._lib import lib, check, ptr, stream_of
+from tests import _data as D
+from tests.test_gpu_dp import _model, _setup
+st = stream_of(torch.device("cuda", 0))
+res = {}
+for path in ("dp", "single"):
+    m = _model()
+    ex = _setup(m, 2)
+    am, av = torch.zeros_like(m.flat), torch.zeros_like(m.flat)
+    loss = torch.empty(1, device="cuda")
+    c = MC.Comm(0, 2, bytes(128), 0) if path == "dp" else None   # stub "world 2": grad_scale 1/2
+    losses = []
+    for t in range(1, 4):
+        x = D.triplets(2, 3, 64, 128, seed=10 + t).float().cuda().contiguous()
+        if path == "dp":
+            check(lib().md2_model_train_step_dp(ex.handle, c.handle, ptr(x), None, ptr(am), ptr(av),
+                                                1e-3, 0.9, 0.999, 1e-8, t, ptr(loss), st), "train_step_dp")
+        else:
+            check(lib().md2_model_train_step(ex.handle, ptr(x), None, ptr(am), ptr(av), 1e-3, t,
+                                             ptr(loss), st), "train_step")
+        torch.cuda.synchronize()
+        losses.append(loss.item())
+    if c is not None:
+        calls, nbytes = c.stats()
+        assert calls == 3 * ex.nseg and nbytes == 3 * 4 * m.numel, (calls, nbytes)
+        assert c.query() == (0, 2)
+        c.close()
+    for k, v in (("flat", m.flat), ("m", am), ("v", av)):
+        res[f"{path}_{k}"] = v.cpu().numpy()
+    res[f"{path}_loss"] = np.array(losses)
+np.savez(out, **res)
+print("SEG_OK")
+"""
+
+
+@pytest.mark.timeout(240)
+def test_c_train_steps_segment_update_bitwise(tmp_path):
+    """the C entry points' per-segment update paths -- md2_model_train_step_dp with a
+    communicator (each bucket's ADAM + re-pack on the update stream after its all-reduce; here the
+    recording stub at "world 2", so grad_scale = 1/2 and no values change in the collective) and
+    md2_model_train_step -- give the same parameters, ADAM moments and losses bit for bit with
+    MD2_SEG_UPDATE=1 as with the default single update, over three steps that each read the
+    previous step's re-packed weights.  Also: md2_comm_stats counts one all-reduce per segment
+    with the whole gradient's bytes, md2_comm_rank reports the communicator's (rank, size)."""
+    import subprocess
+    import sys
+    import numpy as np
+    root, so = _stub_lib()
+    outs = {}
+    for seg in ("0", "1"):
+        out = str(tmp_path / f"seg{seg}.npz")
+        env = dict(os.environ, MD2_RCCL_LIB=so, MD2_TUNING="1", MD2_SEG_UPDATE=seg)
+        r = subprocess.run([sys.executable, "-c", _SEG_CHILD, root, out], env=env, capture_output=True,
+                           text=True, timeout=200)
+        assert r.returncode == 0 and "SEG_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+        outs[seg] = np.load(out)
+    for k in outs["0"].files:
+        assert np.array_equal(outs["0"][k], outs["1"][k]), k
+    assert not np.array_equal(outs["0"]["dp_flat"], outs["0"]["single_flat"])   # scale 1/2 differs

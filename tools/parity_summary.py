@@ -9,6 +9,11 @@ import sys
 
 src = sys.argv[1] if len(sys.argv) > 2 else "gpurun_out/parity"
 out = sys.argv[2] if len(sys.argv) > 2 else sys.argv[1]
+if len(sys.argv) < 2 or os.path.isfile(src) or os.path.exists(out) or not os.path.isdir(src):
+    # the output must be a NEW file: a committed record passed as the only argument would
+    # otherwise be overwritten by the summary of gpurun_out/parity
+    sys.exit(f"usage: parity_summary.py [PARITY_DIR] NEW_OUT.json  (refusing: src={src!r}, out={out!r} "
+             "exists or src is not a directory)")
 recs = {}
 for f in sorted(glob.glob(os.path.join(src, "*.json"))):
     d = json.load(open(f))
