@@ -84,6 +84,13 @@ CASES = [
     ((4, 8, 130, 256), 1, 3, 1, 1, False, None, True),           # zero padding, strip fwd/wgrad
     ((1, 16, 4, 64), 1, 3, 1, 1, True, "sigmoid", True),
     ((2, 64, 32, 104), 1, 3, 1, 1, True, "sigmoid", True),
+    # LDS-halo kernel (conv_halo.inc) edges: a 256-pixel tile spanning many small images (W = 7:
+    # 40 halo rows), ragged N, C = 32 (two channel chunks, split-K of one), M = 128 (two row
+    # tiles), a map too wide for the halo image (W = 200: conv_px3 instead)
+    ((5, 64, 5, 7), 64, 3, 1, 1, False, None, False),
+    ((3, 32, 13, 97), 128, 3, 1, 1, False, "relu", True),
+    ((2, 128, 9, 29), 128, 3, 1, 1, False, None, False),
+    ((2, 64, 6, 200), 64, 3, 1, 1, False, None, False),
     # every conv of the benchmarked step (BASELINE config 3: B=12 triplets, 416x128) at its bench
     # shape -- the encoder on 36 frames, the pose decoder on 24 pairs, the depth decoder on the 12
     # targets -- so each planner choice the bench runs (tile, split-K count, stride-2 phase launch,
