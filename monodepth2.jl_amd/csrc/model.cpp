@@ -1792,6 +1792,13 @@ int model_debug_tensor(Model* m, int index, const char** name, const void** ptr,
     if (m->d_skip[f])
       ts.push_back({"d_skip" + std::to_string(f), m->d_skip[f], N, m->featC[f], m->featH[f],
                     m->featW[f], 0});
+  // DepthDecoder intermediates of the last forward (forward-accuracy bisection, tools/forward_bisect.py)
+  for (auto& d : m->br) {
+    const std::string pre = "depth.branch" + std::to_string(d.b.bid);
+    ts.push_back({pre + ".c1", d.o1, m->ND, d.b.cout, d.h, d.w, 0});
+    ts.push_back({pre + ".up", d.up, m->ND, d.b.cout, 2 * d.h, 2 * d.w, 0});
+    ts.push_back({pre + ".c2", d.o2, m->ND, d.b.cout, 2 * d.h, 2 * d.w, 0});
+  }
   ts.push_back({"d_mp", m->d_mp, B, 64, m->Hm, m->Wm, 0});
   ts.push_back({"d_f0", m->d_f0, B, 64, m->H0, m->W0, 0});
   if (index < 0 || index >= (int)ts.size()) {

@@ -744,14 +744,20 @@ class Adam:
 
 
 def slow_depth_loss(disp, rvecs, tvecs, x, K, invK, source_ids=(1, 3), target_id=2,
-                    min_depth=0.1, max_depth=100.0, forced_sel=None, per_source=None):
+                    min_depth=0.1, max_depth=100.0, forced_sel=None, per_source=None,
+                    forced_cells=None):
     """Loss inside the ``gradient(theta)`` closure of ``slow_depth`` (src/simple_depth.jl:25-41):
     mean(prediction_loss) + smooth_loss(disp) (no 1e-3 weight, no mean normalisation).
-    ``forced_sel`` / ``per_source``: the test hooks of ``loss_from_outputs``."""
+    ``forced_sel`` / ``per_source`` / ``forced_cells`` ([2, N, H, W]: the imposed bilinear cells,
+    border states and L1 signs): the test hooks of ``loss_from_outputs``."""
     Ps = [composeT(r, t, sid < target_id) for r, t, sid in zip(rvecs, tvecs, source_ids)]
-    warped = warp(disp, x, Ps, K, invK, source_ids, min_depth, max_depth)
+    warped = warp(disp, x, Ps, K, invK, source_ids, min_depth, max_depth, cells=forced_cells)
     target_x = x[:, target_id - 1]
-    src_losses = [photometric_loss(p, target_x) for p in warped]
+    if forced_cells is None:
+        src_losses = [photometric_loss(p, target_x) for p in warped]
+    else:
+        src_losses = [photometric_loss(p, target_x, l1_sign=forced_l1_sign(forced_cells[j], p.shape[1]))
+                      for j, p in enumerate(warped)]
     if per_source is not None:
         per_source.append([l.detach() for l in src_losses])
     pred = _forced_min(src_losses, forced_sel) if forced_sel is not None else _first_argmin(src_losses)

@@ -191,25 +191,86 @@ def _oracle_grad(g, dt, arch, levels, target_id, source_ids, at_gpu=False, jitte
     return f.grad.double(), fwd, lo.item(), spec
 
 
+def _to_dev(v, dev):
+    if isinstance(v, torch.Tensor):
+        return v.to(dev)
+    if isinstance(v, dict):
+        return {k: _to_dev(x, dev) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return type(v)(_to_dev(x, dev) for x in v)
+    return v
+
+
+def _oracle_grad_torch_gpu(g, dt, **kw):
+    """The same oracle evaluated by torch ON THE GPU (MIOpen / rocBLAS kernels, TF32 off): a second,
+    independent fp32 implementation of the reference, as the CPU one (oneDNN) is a first."""
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.deterministic = True     # the same realisation on every run
+    torch.backends.cudnn.benchmark = False
+    gd = _to_dev({k: v for k, v in g.items() if k not in ("grad", "flat_out")}, "cuda")
+    with torch.device("cuda"):
+        grad, fwd, loss, spec = _oracle_grad(gd, dt, **kw)
+    torch.cuda.synchronize()
+    return grad.cpu(), ([d.cpu() for d in fwd[0]], fwd[1].cpu()), loss, spec
+
+
+def permute_samples(g, perm):
+    """g (run()'s record) with its N samples reordered by ``perm``: the loss is a mean over
+    samples, pixels and scales and BatchNorm's statistics are sums over the batch, so the exact
+    loss and gradient are unchanged while every batch-level reduction adds in another order -- an
+    independent fp32 rounding realisation of the same function (mono mode only)."""
+    perm = torch.as_tensor(perm, dtype=torch.long)
+    N = perm.numel()
+    out = dict(g)
+    out["x"] = g["x"][perm]
+    L = g["x"].shape[1]
+    dec = {}
+    for k, v in g["decisions"].items():
+        if k.startswith("pose"):
+            dec[k] = v[perm]
+        else:                                          # encoder, n-major [N*L, ...]
+            dec[k] = v.reshape(N, L, *v.shape[1:])[perm].reshape(v.shape)
+    out["decisions"] = dec
+    out["sel"] = g["sel"][:, perm]
+    out["cells"] = g["cells"][:, :, perm]
+    out["disps"] = [d[perm] for d in g["disps"]]
+    out["pose"] = g["pose"].reshape(2, N, 6)[:, perm].reshape(2 * N, 6)
+    return out
+
+
+def _fwd_floors(spec, g32, f32, l32, g64, f64, l64):
+    fl = per_tensor(spec, g32, g64)
+    for s_, (a, b) in enumerate(zip(f32[0], f64[0])):
+        fl[f"__disp{s_}"] = D.rel_err(a, b)
+    fl["__pose"] = D.rel_err(f32[1], f64[1])
+    fl["__loss"] = abs(l32 - l64) / abs(l64)
+    return fl
+
+
 def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_ids=(1, 3)):
     """References for judging the GPU train step, all from the oracle with every GPU decision
-    imposed.  The GPU gradient differs from the fp64 oracle's for two reasons, checked apart:
-      forward   the GPU's disparities / poses carry fp32 rounding (tested directly, 1e-5), and
-                the loss tail's gradient is sensitive to them (cancelling sums: a head's bias
-                gradient sums ~1e6 pixel gradients of both signs, and the smoothness term's mean
-                normalisation makes it scale invariant);
-      backward  given its own forward point, the GPU backward must reproduce the exact gradient:
-                ``sub`` = the fp64 oracle with the loss tail evaluated AT the GPU's outputs.
-    Returns a dict:
-      floor[k]      per-tensor error of the same oracle in fp32 vs fp64 (end to end), plus the
-                    forward outputs' floors "__disp<s>", "__pose", "__loss";
-      floor_b[k]    fp32 vs fp64 of ``sub`` (the backward's own fp32 floor), the larger of two
-                    fp32 realisations (as is, and with the constants jittered by +-1 ulp);
+    imposed.
+      floor[k]      the end-to-end fp32 FLOOR of tensor k: the error against fp64 of a plain fp32
+                    evaluation of the reference, taken as the larger of two independent ones --
+                    the oracle in fp32 on the CPU (torch/oneDNN, ``floor_cpu32``) and the same
+                    oracle in fp32 by torch on the GPU (MIOpen, ``floor_gpu32``).  One evaluation
+                    is one sample of that error, and for the cancelling sums (a head's bias
+                    gradient sums ~1e6 pixel gradients of both signs) the samples scatter by up to
+                    40x (tools/fp32_realizations.py, profiles/r05_fp32_realizations.json) -- so the
+                    GPU realisation is taken three times: as is and with the batch's samples
+                    reordered twice (the same exact function; every batch-level sum adds in
+                    another order);
+                    plus the forward outputs' floors "__disp<s>", "__pose", "__loss";
+      floor_b[k]    fp32 vs fp64 of ``sub`` -- the oracle with its loss tail evaluated AT the
+                    GPU's forward outputs, i.e. the exact gradient the GPU backward must reproduce
+                    (the larger of two fp32 realisations: as is, and with the constants jittered
+                    by +-1 ulp);
       coherent[k]   |sub(K, invK, poses each +-1 fp32 ulp) - sub| / |sub|: the sensitivity to a
-                    coherent warp perturbation of the size of the GPU's fp32 warp constants
-                    (the per-(sample, source) maps every pixel shares) -- large exactly for the
-                    cancelling sums (a head's bias gradient);
-      explained[k]  |sub - oracle| / |oracle|: what the forward's rounding alone explains;
+                    coherent perturbation of the per-(sample, source) warp maps of the size of the
+                    GPU's fp32 warp constants;
+      explained[k]  |sub - oracle| / |oracle|: how far the exact gradient moves between the GPU's
+                    forward point and the fp64 one (recorded, not used in any bound);
       bwd[k]        |gpu - sub| / |sub|: the GPU backward's error at its own forward point."""
     kw = dict(arch=arch, levels=levels, target_id=target_id, source_ids=source_ids)
     if o is None:
@@ -219,11 +280,23 @@ def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_i
         spec = O.param_spec(arch, g["x"].shape[2], tuple(levels),
                             embedding_levels=21 if g.get("bins") is not None else 0)
     g32, f32, l32, _ = _oracle_grad(g, torch.float32, **kw)
-    floor = per_tensor(spec, g32, g64)
-    for s_, (a, b) in enumerate(zip(f32[0], f64[0])):
-        floor[f"__disp{s_}"] = D.rel_err(a, b)
-    floor["__pose"] = D.rel_err(f32[1], f64[1])
-    floor["__loss"] = abs(l32 - l64) / abs(l64)
+    floor_cpu = _fwd_floors(spec, g32, f32, l32, g64, f64, l64)
+    # torch-on-GPU realisations: as is, and with the samples reordered twice (the same exact
+    # function; every batch-level sum adds in another order) -- mono mode with N >= 2
+    N = g["x"].shape[0]
+    perms = [None]
+    if g.get("bins") is None and N >= 2:
+        perms += [list(range(N))[::-1], list(range(1, N)) + [0]]
+    floor_gpu_r = []
+    for perm in perms:
+        gp = g if perm is None else permute_samples(g, perm)
+        gg32, gf32, gl32, _ = _oracle_grad_torch_gpu(gp, torch.float32, **kw)
+        if perm is not None:   # forward outputs back in the original sample order
+            inv = torch.argsort(torch.as_tensor(perm))
+            gf32 = ([d[inv] for d in gf32[0]], gf32[1].reshape(2, N, 6)[:, inv].reshape(2 * N, 6))
+        floor_gpu_r.append(_fwd_floors(spec, gg32, gf32, gl32, g64, f64, l64))
+    floor_gpu = {k: max(f[k] for f in floor_gpu_r) for k in floor_cpu}
+    floor = {k: max(floor_cpu[k], floor_gpu[k]) for k in floor_cpu}
     s64, _, _, _ = _oracle_grad(g, torch.float64, at_gpu=True, **kw)
     s32, _, _, _ = _oracle_grad(g, torch.float32, at_gpu=True, **kw)
     sj, _, _, _ = _oracle_grad(g, torch.float64, at_gpu=True, jitter=11, **kw)
@@ -232,20 +305,22 @@ def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_i
     s32j, _, _, _ = _oracle_grad(g, torch.float32, at_gpu=True, jitter=11, **kw)
     fb = per_tensor(spec, s32, s64)
     fbj = per_tensor(spec, s32j, sj)
-    return {"floor": floor, "floor_b": {k: max(fb[k], fbj[k]) for k in fb},
+    return {"floor": floor, "floor_cpu32": floor_cpu, "floor_gpu32": floor_gpu,
+            "floor_b": {k: max(fb[k], fbj[k]) for k in fb},
             "explained": per_tensor(spec, s64, g64), "coherent": per_tensor(spec, sj, s64),
             "bwd": per_tensor(spec, g["grad"].double(), s64)}
 
 
-# Ceilings on the adaptive bounds below, no sensitivity multiplier beyond
-# the fp32 floor itself: the GPU must be as accurate as a plain fp32 evaluation of the reference
-# (the oracle run in fp32 -- `floor_b` at the GPU's forward point, `floor` / `explained` end to
-# end) and, where fp32 itself does better, within an absolute 1e-4 (backward) / 1e-3 (end to end).
-# The absolute values alone cannot be met by ANY fp32 evaluation on textured inputs: the oracle's
-# own fp32-vs-fp64 floor of the encoder's BN gradients is ~1e-3 at B=12 416x128 and ~1e-1 for
-# ResNet-50 at 640x192 (profiles/r04_parity.json), because those gradients are cancelling sums.
-# Measured worst ratios (r04): backward 1.61 x max(1e-4, floor_b), end to end 1.09 x
-# max(1e-3, floor, explained).
+# Bounds (anchored on the fp32 floor, no term that grows with the GPU's own
+# forward deviation):
+#   forward     disparities per scale, poses: within max(1e-6, 2 x the fp32 floor);
+#               loss within max(1e-6, 4 x floor);
+#   end to end  every parameter tensor within max(1e-3, 4 x its fp32 floor) -- 1e-3 because no
+#               fp32 evaluation meets less on the encoder's BN gradients (cancelling sums; both
+#               fp32 realisations reach ~1e-3 there at B=12 416x128);
+#   backward    (at the GPU's own forward point) within max(4 x floor_b, 4 x coherent, 2e-5; 1e-4
+#               for the Cout=1 heads' bias gradients) and never above max(1e-4, 2 x floor_b,
+#               1.25 x coherent).
 # Named exception (backward): `coherent`, the move of the EXACT gradient under a +-1-ulp jitter of
 # the fp32 camera inputs (K, K^-1, poses).  Any fp32 pipeline rounds the per-(sample, source)
 # warp maps once, which perturbs every pixel's warp coherently; the decoder's low-resolution
@@ -253,16 +328,16 @@ def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_i
 # 640x192 their coherent sensitivity (1.6e-4, profiles/r04_parity_r50.json) exceeds the absolute
 # 1e-4.  The backward ceiling admits 1.25 x coherent for those tensors and nothing more.
 CEIL_BWD, CEIL_BWD_FLOOR, CEIL_BWD_COHERENT = 1e-4, 2.0, 1.25
-CEIL_E2E, CEIL_E2E_FLOOR = 1e-3, 1.25
+E2E_ABS, E2E_FLOOR = 1e-3, 4.0
+FWD_ABS, FWD_FLOOR = 1e-6, 2.0
 
 
 def _head_bias(k):
     return k.startswith("depth.head") and k.endswith(".bias")
 
 
-def _ceilings(b, floor, k):
-    return (max(CEIL_BWD, CEIL_BWD_FLOOR * b["floor_b"][k], CEIL_BWD_COHERENT * b["coherent"][k]),
-            max(CEIL_E2E, CEIL_E2E_FLOOR * max(floor[k], b["explained"][k])))
+def _ceil_bwd(b, k):
+    return max(CEIL_BWD, CEIL_BWD_FLOOR * b["floor_b"][k], CEIL_BWD_COHERENT * b["coherent"][k])
 
 
 def parity_record_path(label):
@@ -276,21 +351,20 @@ def parity_record_path(label):
 
 def check_step(g, o, errs, b, label=""):
     """The full-step assertions shared by the model parity tests (b = oracle_bounds(g, o)):
-      * loss within max(1e-6, 4 x its fp32 floor); disparities / poses within max(1e-5, 4 x floor);
+      * loss within max(1e-6, 4 x its fp32 floor); disparities (per scale) / poses within
+        max(1e-6, 2 x their fp32 floor);
       * BACKWARD, per tensor: |gpu - sub| within max(4 x the backward's fp32 floor, 4 x its coherent
-        warp-constant sensitivity, 2e-5; 1e-4 for the cancelling head biases) -- the GPU reproduces the exact gradient at its own
-        forward point -- and never above max(1e-4, 2 x floor_b, 1.25 x coherent);
-      * END TO END, per tensor: |gpu - oracle| within max(4 x the fp32 floor, 2 x what the
-        forward's rounding explains, the backward bound + what the forward explains, 2e-5), and
-        never above max(1e-3, 1.25 x max(floor, explained)).
-    Every tensor's (err, bound, floor, explained, coherent) is written to parity_record_path(label)
+        warp-constant sensitivity, 2e-5; 1e-4 for the cancelling head biases) -- the GPU reproduces
+        the exact gradient at its own forward point -- and never above max(1e-4, 2 x floor_b,
+        1.25 x coherent);
+      * END TO END, per tensor: |gpu - oracle| within max(1e-3, 4 x the fp32 floor).
+    Every tensor's (err, bound, floors, explained, coherent) is written to parity_record_path(label)
     before anything is asserted."""
     floor = b["floor"]
-    assert abs(g["loss"] - o["loss"]) <= max(1e-6, 4 * floor["__loss"]) * abs(o["loss"]), \
-        (g["loss"], o["loss"], floor["__loss"])
+    fwd = {"__loss": (abs(g["loss"] - o["loss"]) / abs(o["loss"]), max(1e-6, 4 * floor["__loss"]))}
     for s_, (a, r) in enumerate(zip(g["disps"], o["disps"])):
-        assert D.rel_err(a, r) < max(1e-5, 4 * floor[f"__disp{s_}"]), s_
-    assert D.rel_err(g["pose"], o["pose"]) < max(1e-5, 4 * floor["__pose"])
+        fwd[f"__disp{s_}"] = (D.rel_err(a, r), max(FWD_ABS, FWD_FLOOR * floor[f"__disp{s_}"]))
+    fwd["__pose"] = (D.rel_err(g["pose"], o["pose"]), max(FWD_ABS, FWD_FLOOR * floor["__pose"]))
     # named exception: a Cout=1 head's bias gradient is ONE sum over N*H*W per-pixel gradients of
     # both signs (cancelling 10-1000x), so its relative error is the per-pixel fp32 rounding of
     # the head's input gradient amplified by the cancellation -- the GPU's and the fp32 oracle's
@@ -299,34 +373,42 @@ def check_step(g, o, errs, b, label=""):
     # backward ceiling (1e-4) instead of 4 x floor_b
     bb = {k: max(4 * b["floor_b"][k], 4 * b["coherent"][k], 2e-5, CEIL_BWD if _head_bias(k) else 0.0)
           for k in b["bwd"]}
-    # end to end <= backward error + what the forward's rounding explains (triangle inequality)
-    be = {k: max(4 * floor[k], 2 * b["explained"][k], bb[k] + b["explained"][k], 2e-5) for k in errs}
+    be = {k: max(E2E_ABS, E2E_FLOOR * floor[k]) for k in errs}
     rec = {"label": label, "loss_gpu": g["loss"], "loss_oracle": o["loss"],
-           "loss_rel_err": abs(g["loss"] - o["loss"]) / abs(o["loss"]), "loss_floor": floor["__loss"],
+           "loss_rel_err": fwd["__loss"][0], "loss_floor": floor["__loss"],
            "disp_rel_err": [D.rel_err(a, r) for a, r in zip(g["disps"], o["disps"])],
-           "pose_rel_err": D.rel_err(g["pose"], o["pose"]),
-           "ceilings": {"backward": [CEIL_BWD, CEIL_BWD_FLOOR, CEIL_BWD_COHERENT], "end_to_end": [CEIL_E2E, CEIL_E2E_FLOOR]},
-           "tensors": {k: {"bwd_err": b["bwd"][k], "bwd_bound": bb[k], "bwd_ceiling": _ceilings(b, floor, k)[0],
-                           "e2e_err": errs[k], "e2e_bound": be[k], "e2e_ceiling": _ceilings(b, floor, k)[1],
-                           "floor": floor[k], "floor_b": b["floor_b"][k], "explained": b["explained"][k],
+           "disp_floor": [floor[f"__disp{s_}"] for s_ in range(len(g["disps"]))],
+           "disp_floor_cpu32": [b["floor_cpu32"][f"__disp{s_}"] for s_ in range(len(g["disps"]))],
+           "disp_floor_gpu32": [b["floor_gpu32"][f"__disp{s_}"] for s_ in range(len(g["disps"]))],
+           "pose_rel_err": fwd["__pose"][0], "pose_floor": floor["__pose"],
+           "forward": {k: {"err": e, "bound": bd} for k, (e, bd) in fwd.items()},
+           "bounds": {"end_to_end": [E2E_ABS, E2E_FLOOR], "forward": [FWD_ABS, FWD_FLOOR],
+                      "backward_ceiling": [CEIL_BWD, CEIL_BWD_FLOOR, CEIL_BWD_COHERENT]},
+           "tensors": {k: {"bwd_err": b["bwd"][k], "bwd_bound": bb[k], "bwd_ceiling": _ceil_bwd(b, k),
+                           "e2e_err": errs[k], "e2e_bound": be[k],
+                           "floor": floor[k], "floor_cpu32": b["floor_cpu32"][k], "floor_gpu32": b["floor_gpu32"][k],
+                           "floor_b": b["floor_b"][k], "explained": b["explained"][k],
                            "coherent": b["coherent"][k]} for k in errs}}
     rec["worst_bwd"] = max(rec["tensors"].items(), key=lambda kv: kv[1]["bwd_err"])[0]
     rec["worst_e2e"] = max(rec["tensors"].items(), key=lambda kv: kv[1]["e2e_err"])[0]
+    rec["worst_e2e_over_floor"] = max(v["e2e_err"] / max(v["floor"], 1e-30) for v in rec["tensors"].values())
     with open(parity_record_path(label), "w") as f:
         json.dump(rec, f, indent=1)
     rb = sorted(((b["bwd"][k] / bb[k], k) for k in bb), reverse=True)
     re_ = sorted(((errs[k] / be[k], k) for k in be), reverse=True)
-    print(f"\n{label} loss {g['loss']:.7f} vs {o['loss']:.7f}; backward (gpu vs oracle at gpu outputs): " +
+    print(f"\n{label} loss {g['loss']:.7f} vs {o['loss']:.7f}; forward " +
+          ", ".join(f"{k} {e:.1e}/{bd:.1e}" for k, (e, bd) in fwd.items()) +
+          "; backward (gpu vs oracle at gpu outputs): " +
           ", ".join(f"{k} {b['bwd'][k]:.1e}/{bb[k]:.1e} (floor {b['floor_b'][k]:.1e}, coherent {b['coherent'][k]:.1e})"
                     for _, k in rb[:3]) + "; end to end: " +
-          ", ".join(f"{k} {errs[k]:.1e}/{be[k]:.1e} (floor {floor[k]:.1e}, explained {b['explained'][k]:.1e})"
+          ", ".join(f"{k} {errs[k]:.1e}/{be[k]:.1e} (floor cpu32 {b['floor_cpu32'][k]:.1e} gpu32 {b['floor_gpu32'][k]:.1e})"
                     for _, k in re_[:3]))
+    bad = {k: v for k, v in fwd.items() if v[0] > v[1]}
+    assert not bad, ("forward", bad)
     bad = {k: (b["bwd"][k], bb[k]) for k in bb if b["bwd"][k] > bb[k]}
     assert not bad, ("backward", bad)
+    bad = {k: (b["bwd"][k], _ceil_bwd(b, k)) for k in bb if b["bwd"][k] > _ceil_bwd(b, k)}
+    assert not bad, ("backward above its ceiling", bad)
     bad = {k: (errs[k], be[k]) for k in be if errs[k] > be[k]}
     assert not bad, ("end to end", bad)
-    bad = {k: (b["bwd"][k], _ceilings(b, floor, k)[0]) for k in bb if b["bwd"][k] > _ceilings(b, floor, k)[0]}
-    assert not bad, ("backward above its ceiling", bad)
-    bad = {k: (errs[k], _ceilings(b, floor, k)[1]) for k in errs if errs[k] > _ceilings(b, floor, k)[1]}
-    assert not bad, ("end to end above its ceiling", bad)
     return max(errs.values())

@@ -7,8 +7,11 @@ oracle's restatement (oracle/md2_oracle.py slow_depth_loss, Adam).
   strict tier (affine source frames): loss rel 2e-5, gradients rel 2e-4;
 * ``md2_adam`` against the oracle's Flux ADAM rule (rel 1e-6 over three steps);
 * 8-iteration ADAM(3e-4) trajectories against the fp64 oracle loop: per-iteration loss rel
-  1e-4; from a textured start also the disparity update direction (cosine > 0.99) and the pose
-  updates (rel 2e-2).  ADAM's first steps are ~lr*sign(g), so pixels with |g| near fp32
+  1e-4; from a textured start, with the GPU's branch decisions of every iteration imposed on
+  the oracle loop, the loss (1e-5), the disparity update direction and the pose updates within
+  4x the same loop run in fp32 (CPU and torch-on-GPU);
+* the reference's 500 iterations at 416x128 against the committed fp64 trajectory, bounded by
+  4x the drift of the fp32 oracle loop (tests/golden/slow_depth_traj_416x128.npz).  ADAM's first steps are ~lr*sign(g), so pixels with |g| near fp32
   rounding may legitimately step the other way; the aggregate checks are what is stable.
 """
 import pytest
@@ -91,14 +94,21 @@ def test_adam_op_matches_flux_rule():
     assert D.rel_err(p.cpu(), ref) < 1e-6
 
 
-def _oracle_loop(disp, rv, tv, x, K, invK, iters):
+def _oracle_loop(disp, rv, tv, x, K, invK, iters, decisions=None):
+    """The reference loop (src/simple_depth.jl:22-42) on the oracle; ``decisions`` (per
+    iteration: the GPU's (sel, cells)) imposes the GPU's per-pixel source choice and bilinear
+    cells / border states / L1 signs iteration by iteration."""
     opt = O.Adam(eta=3e-4)
     losses = []
-    for _ in range(iters):
+    for it in range(iters):
         disp.requires_grad_(True)
         for t in rv + tv:
             t.requires_grad_(True)
-        loss = O.slow_depth_loss(disp, rv, tv, x, K, invK)
+        kw = {}
+        if decisions is not None:
+            sel, cells = decisions[it]
+            kw = dict(forced_sel=sel.to(disp.device), forced_cells=cells.to(disp.device))
+        loss = O.slow_depth_loss(disp, rv, tv, x, K, invK, **kw)
         loss.backward()
         losses.append(loss.item())
         with torch.no_grad():
@@ -111,32 +121,151 @@ def _oracle_loop(disp, rv, tv, x, K, invK, iters):
     return disp, rv, tv, losses
 
 
+def _oracle_loop_torch_gpu(disp, rv, tv, x, K, invK, iters, decisions=None):
+    """The same fp32 oracle loop evaluated by torch on the GPU: an independent fp32 rounding
+    realisation of the reference loop (different reduction orders than the CPU's)."""
+    dev = lambda t: t.float().cuda()
+    with torch.device("cuda"):
+        d, r, t, losses = _oracle_loop(dev(disp), [dev(a) for a in rv], [dev(a) for a in tv], dev(x),
+                                       dev(K), dev(invK), iters, decisions)
+    torch.cuda.synchronize()
+    return d.cpu(), [a.cpu() for a in r], [a.cpu() for a in t], losses
+
+
+def _gpu_steps_recording(sd, iters):
+    """sd.step() x iters, recording each iteration's branch decisions (vis_sel, vis_cell)."""
+    from md2hip.slow_depth import adam_update
+    losses, dec = [], []
+    nd = sd.N * sd.H * sd.W
+    for _ in range(iters):
+        r = sd.evaluate(visualize=True)
+        sd.grad[:nd].copy_(r["d_disp"][0].reshape(-1))
+        sd.grad[nd:].copy_(r["d_pose"].reshape(-1))
+        sd.t += 1
+        adam_update(sd.theta, sd.grad, sd.m, sd.v, sd.t, sd.lr)
+        losses.append(r["loss"].item())
+        dec.append((r["vis_sel"][0].cpu().unsqueeze(1).long(), r["vis_cell"][0].cpu()))
+    return losses, dec
+
+
 @pytest.mark.parametrize("textured_theta", [False, True], ids=["reference-init", "textured"])
 def test_slow_depth_trajectory(textured_theta):
     """8 ADAM(3e-4) iterations vs the fp64 oracle loop.  From the reference's own init the
     disparity gradient is rounding noise (pure rotation, see above), so ADAM's first disparity
     steps are noise-driven there -- in the Julia reference as well -- and only the loss
-    trajectory is compared; from a textured start the disparity update direction is too."""
+    trajectory is compared.  From a textured start the GPU's branch decisions (per-pixel source
+    choice, bilinear cells, border states, L1 signs) are recorded EVERY iteration and imposed on
+    the oracle loop (tools/pose_grad_acc.py: at this start a few warped coordinates sit on grid
+    lines, and the cell the GPU's fp32 coordinate falls in, a valid subgradient, moves d_pose by
+    6.5e-3 against fp64's choice; with the cells imposed the GPU's d_pose error is 1-2e-5, below
+    the fp32 oracle's 3e-5); then the disparity update direction (cosine) and the pose update are
+    held to 4x the same loop run in fp32 (CPU and torch-on-GPU realisations)."""
     sd, x, K, invK = _setup(1, 64, 128, seed=5, strict=False, textured_theta=textured_theta)
     disp0 = sd.disp.detach().double().cpu().clone()
     rows = sd.pose_rows.detach().double().cpu().clone()
     iters = 8
-    gl = [sd.step().item() for _ in range(iters)]
-    disp, rv, tv, ol = _oracle_loop(disp0.clone(), [rows[s:s + 1, :3].clone() for s in range(2)],
-                                    [rows[s:s + 1, 3:].clone() for s in range(2)], x, K, invK, iters)
+    start = lambda: (disp0.clone(), [rows[s:s + 1, :3].clone() for s in range(2)],
+                     [rows[s:s + 1, 3:].clone() for s in range(2)])
+    if not textured_theta:
+        gl = [sd.step().item() for _ in range(iters)]
+        _, _, _, ol = _oracle_loop(*start(), x, K, invK, iters)
+        for a, b in zip(gl, ol):
+            assert abs(a - b) <= 1e-4 * abs(b), (gl, ol)
+        return
+    gl, dec = _gpu_steps_recording(sd, iters)
+    disp, rv, tv, ol = _oracle_loop(*start(), x, K, invK, iters, dec)
     for a, b in zip(gl, ol):
-        assert abs(a - b) <= 1e-4 * abs(b), (gl, ol)
-    if textured_theta:
-        dg = (sd.disp.detach().double().cpu() - disp0).reshape(-1)
-        do = (disp - disp0).reshape(-1)
-        cos = torch.dot(dg, do) / (dg.norm() * do.norm())
-        assert cos > 0.99, cos.item()
-        pg = sd.pose_rows.detach().double().cpu() - rows
-        po = torch.cat([torch.cat([r, t], 1) for r, t in zip(rv, tv)], 0) - rows
-        import json
-        from tests._model_parity import parity_record_path
-        per = (pg - po).abs() / po.abs().clamp_min(1e-30)
-        with open(parity_record_path("slow_depth_trajectory"), "w") as f:
-            json.dump({"loss_gpu": gl, "loss_oracle": ol, "disp_update_cos": cos.item(),
-                       "pose_update_rel_err": D.rel_err(pg, po), "pose_update_per_entry": per.tolist()}, f, indent=1)
-        assert D.rel_err(pg, po) < 2e-2
+        assert abs(a - b) <= 1e-5 * abs(b), (gl, ol)
+    dg = (sd.disp.detach().double().cpu() - disp0).reshape(-1)
+    do = (disp - disp0).reshape(-1)
+    cosf = lambda a, b: (torch.dot(a, b) / (a.norm() * b.norm())).item()
+    cos = cosf(dg, do)
+    pg = sd.pose_rows.detach().double().cpu() - rows
+    po = torch.cat([torch.cat([r, t], 1) for r, t in zip(rv, tv)], 0) - rows
+    per = (pg - po).abs() / po.abs().clamp_min(1e-30)
+    # the floor: the same 8 iterations with the same imposed decisions, run in fp32 -- the
+    # oracle on the CPU and by torch on the GPU -- against fp64
+    pfl, cfl = [], []
+    for lp in (_oracle_loop, _oracle_loop_torch_gpu):
+        d0, r0, t0 = start()
+        d32, rv32, tv32, _ = lp(d0.float(), [a.float() for a in r0], [a.float() for a in t0], x.float(),
+                                K.float(), invK.float(), iters, dec)
+        p32 = torch.cat([torch.cat([r, t], 1) for r, t in zip(rv32, tv32)], 0).double() - rows
+        pfl.append(D.rel_err(p32, po))
+        cfl.append(1 - cosf((d32.double() - disp0).reshape(-1), do))
+    import json
+    from tests._model_parity import parity_record_path
+    with open(parity_record_path("slow_depth_trajectory"), "w") as f:
+        json.dump({"loss_gpu": gl, "loss_oracle": ol, "disp_update_cos": cos, "disp_update_1mcos_fp32": cfl,
+                   "pose_update_rel_err": D.rel_err(pg, po), "pose_update_fp32_cpu_gpu": pfl,
+                   "pose_update_per_entry": per.tolist()}, f, indent=1)
+    assert 1 - cos <= max(1e-7, 4 * max(cfl)), (cos, cfl)
+    assert D.rel_err(pg, po) < max(1e-5, 4 * max(pfl)), (D.rel_err(pg, po), pfl)
+
+
+def _golden_traj():
+    import os
+    import numpy as np
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "slow_depth_traj_416x128.npz")
+    return np.load(path)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("start", ["reference", "textured"])
+def test_slow_depth_500_iterations_416x128(start):
+    """BASELINE config 1 at the reference's length (src/simple_depth.jl:16-42): 500 ADAM(3e-4)
+    iterations on one 416x128 triplet against the committed fp64 oracle trajectory
+    (tests/golden/make_slow_depth_traj.py).  The bounds are 4x the drift of the same loop run in
+    fp32 -- two plain fp32 evaluations of the reference loop: the oracle on the CPU (stored beside
+    the fp64 one) and the oracle by torch on the GPU (run here): per iteration the loss within 4x
+    the running maximum of their loss deviation (+1e-5); at the end the pose update within 4x
+    their relative error and the disparity update's direction within 4x their (1 - cosine).  From the reference init the disparity gradient starts as rounding noise
+    (a pure rotation: depth cancels), so that loop is chaotic in ANY precision -- the fp32 loop
+    itself ends with 34% pose-update error and cosine 0.54 -- and the bounds say so."""
+    import json
+    import numpy as np
+    from tests._model_parity import parity_record_path
+    z = _golden_traj()
+    sd, x, K, invK = _setup(1, 128, 416, seed=5, strict=False, textured_theta=(start == "textured"))
+    rows0 = sd.pose_rows.detach().double().cpu().clone()
+    disp0 = sd.disp.detach().double().cpu().clone()
+    gl = np.array([sd.step().item() for _ in range(500)])
+    torch.cuda.synchronize()
+    # the second fp32 realisation: the same oracle loop by torch on the GPU (in-test, ~10 s)
+    d_t, rv_t, tv_t, lt = _oracle_loop_torch_gpu(disp0.clone(), [rows0[s:s + 1, :3].clone() for s in range(2)],
+                                                 [rows0[s:s + 1, 3:].clone() for s in range(2)], x, K, invK, 500)
+    l64 = z[f"{start}_loss64"]
+    l32s = [z[f"{start}_loss32"], np.array(lt)]
+    env = np.maximum.accumulate(np.max([np.abs(l - l64) / np.abs(l64) for l in l32s], 0))
+    dev = np.abs(gl - l64) / np.abs(l64)
+    if start == "textured":
+        # per iteration: 4x the fp32 loops' running deviation, plus 1e-5 (one evaluation's loss
+        # accuracy, test_slow_depth_gradient_parity holds 2e-5) for the first steps where both
+        # fp32 loops still sit within a few ulp of fp64
+        lbound = 4 * env + 1e-5
+    else:
+        # from the reference init the loop is driven by rounding noise from step 1: which pixel
+        # steps which way is a property of each realisation, and only the BAND of the deviation
+        # is meaningful -- 4x the largest deviation either fp32 loop shows over the 500 steps
+        lbound = np.full_like(dev, 4 * env[-1])
+    pu_g = sd.pose_rows.detach().double().cpu().numpy() - rows0.numpy()
+    pu64 = z[f"{start}_rows64"] - rows0.numpy()
+    p_t = torch.cat([torch.cat([r, t], 1) for r, t in zip(rv_t, tv_t)], 0).double().numpy()
+    pu32s = [z[f"{start}_rows32"] - rows0.numpy(), p_t - rows0.numpy()]
+    rel = lambda a: float(np.linalg.norm(a - pu64) / np.linalg.norm(pu64))
+    pe, pe32 = rel(pu_g), max(rel(p) for p in pu32s)
+    du_g = (sd.disp.detach().double().cpu() - disp0).numpy().ravel()
+    du64 = z[f"{start}_dupdate64"].ravel().astype(np.float64)
+    du32s = [z[f"{start}_dupdate32"].ravel().astype(np.float64), (d_t.double() - disp0).numpy().ravel()]
+    cos = lambda a, b: float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+    c, c32 = cos(du_g, du64), min(cos(d, du64) for d in du32s)
+    with open(parity_record_path(f"slow_depth_500_{start}"), "w") as f:
+        json.dump({"loss_dev_max": float(dev.max()), "loss_dev_over_bound_max": float((dev / lbound).max()),
+                   "loss_fp32_envelope_final": float(env[-1]), "loss_gpu_final": float(gl[-1]),
+                   "loss_oracle_final": float(l64[-1]), "loss_fp32_final": [float(l[-1]) for l in l32s],
+                   "pose_update_rel_err": pe, "pose_update_fp32": [rel(p) for p in pu32s],
+                   "disp_update_cos": c, "disp_update_cos_fp32": [cos(d, du64) for d in du32s]}, f, indent=1)
+    bad = np.nonzero(dev > lbound)[0]
+    assert bad.size == 0, (bad[:10], dev[bad[:10]], lbound[bad[:10]])
+    assert pe <= max(1e-4, 4 * pe32), (pe, pe32)
+    assert 1 - c <= max(1e-6, 4 * (1 - c32)), (c, c32)
