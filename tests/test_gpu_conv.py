@@ -91,6 +91,14 @@ CASES = [
     ((3, 32, 13, 97), 128, 3, 1, 1, False, "relu", True),
     ((2, 128, 9, 29), 128, 3, 1, 1, False, None, False),
     ((2, 64, 6, 200), 64, 3, 1, 1, False, None, False),
+    # LDS-halo filter gradient (conv_whalo): chunks of 4 rows (80 pixels, 5 k-steps), and of 3
+    # rows (108 pixels + 4 zero pad) with one 32-channel tile and two 64-filter tiles
+    ((3, 64, 12, 20), 64, 3, 1, 1, False, None, False),
+    ((2, 32, 6, 36), 128, 3, 1, 1, False, "relu", True),
+    # reflect-padded dgrad on the halo kernel (the zero-padded adjoint of the (H+2) x (W+2) grid,
+    # then the fold): many small padded images per tile, a 2-row map (every row folds)
+    ((3, 64, 7, 5), 64, 3, 1, 1, True, "elu", True),
+    ((4, 128, 2, 9), 64, 3, 1, 1, True, None, False),
     # every conv of the benchmarked step (BASELINE config 3: B=12 triplets, 416x128) at its bench
     # shape -- the encoder on 36 frames, the pose decoder on 24 pairs, the depth decoder on the 12
     # targets -- so each planner choice the bench runs (tile, split-K count, stride-2 phase launch,

@@ -7,7 +7,7 @@ import re
 import sys
 
 FAMILIES = [
-    ("conv 3x3/1x1/7x7 implicit GEMM (fwd/dgrad/wgrad)", r"conv_(px|px2|px3|px16|wgrad|wgrad_tap|wgrad16|wgrad_stem|wgrad_px3)_kernel"),
+    ("conv 3x3/1x1/7x7 implicit GEMM (fwd/dgrad/wgrad)", r"conv_(px|px2|px3|px16|wgrad|wgrad_tap|wgrad16|wgrad_stem|wgrad_px3|halo3|whalo)_kernel|fold_reflect"),
     ("split-K / wgrad reductions", r"(splitk_reduce|wgrad_reduce)"),
     ("BatchNorm (+ fused stem max pool)", r"bn_|maxpool"),
     ("disparity heads (Cout=1)", r"head_"),
@@ -23,6 +23,7 @@ def main(path, steps=13):
     rows = list(csv.DictReader(open(path)))
     out = {name: 0.0 for name, _ in FAMILIES}
     other = 0.0
+    others = []
     for r in rows:
         t = float(r["TotalDurationNs"]) / steps / 1e3
         for name, pat in FAMILIES:
@@ -31,11 +32,14 @@ def main(path, steps=13):
                 break
         else:
             other += t
+            others.append((t, r["Name"][:100], r["Calls"]))
     total = sum(out.values()) + other
     for name, v in sorted(out.items(), key=lambda x: -x[1]):
         print(f"{v:8.1f} us/step  {100 * v / total:5.1f}%  {name}")
     print(f"{other:8.1f} us/step  {100 * other / total:5.1f}%  other (runtime fills/copies, torch)")
     print(f"{total:8.1f} us/step  total")
+    for t, n, c in sorted(others, reverse=True)[:8]:
+        print(f"    other: {t:8.1f} us/step  calls {c:>6s}  {n}")
 
 
 if __name__ == "__main__":
