@@ -14,6 +14,11 @@ SH = [  # name, x_shape, cout, k, s, p, reflect
     ("l3", (36, 256, 8, 26), 256, 3, 1, 1, 0),
     ("l4.0", (36, 256, 8, 26), 512, 3, 2, 1, 0),
     ("l4", (36, 512, 4, 13), 512, 3, 1, 1, 0),
+    ("d1c1", (12, 512, 4, 13), 256, 3, 1, 1, 1),
+    ("d1c2", (12, 512, 8, 26), 256, 3, 1, 1, 1),
+    ("d2c1", (12, 256, 8, 26), 128, 3, 1, 1, 1),
+    ("d2c2", (12, 256, 16, 52), 128, 3, 1, 1, 1),
+    ("d3c1", (12, 128, 16, 52), 64, 3, 1, 1, 1),
     ("d5c2", (12, 16, 128, 416), 16, 3, 1, 1, 1),
     ("d4c2", (12, 96, 64, 208), 32, 3, 1, 1, 1),
     ("d3c2", (12, 128, 32, 104), 64, 3, 1, 1, 1),
