@@ -467,7 +467,7 @@ def main():
             # the committed PMC profiles are of the default workload (ResNet-18, B=12, 416x128)
             default = (args.arch, B, H, W) == (18, 12, 128, 416)
             traffic, tsrc = pmc_traffic() if default else (None, None)
-            out["roofline"] = {"bound": "mfma", "kernel": "implicit-GEMM zero-padded 3x3 convs (encoder+pose): fwd+dgrad conv_px3, wgrad conv_wgrad_px3 (bf16x6 split products, fp32 sums), + split-K / wgrad reduce",
+            out["roofline"] = {"bound": "mfma", "kernel": "implicit-GEMM zero-padded 3x3 convs (encoder+pose): fwd+dgrad conv_halo3 (LDS halo, stride 1) / conv_px3 (stride 2), wgrad conv_whalo (LDS halo, layers 2-4 + pose) / conv_wgrad_px3 (bf16x6 split products, fp32 sums), + split-K / wgrad reduce",
                                "achieved": round(ach, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
                                "peak_note": "peak = fp32 MFMA (the reference's arithmetic, algorithmic fp32 FLOPs); "

@@ -9,8 +9,8 @@ Writes
   profiles/<tag>_pmc.json           FETCH_SIZE / WRITE_SIZE per launch of the roofline kernels
 
 Roofline kernel set (matches bench.py's HIP-event category 0): implicit-GEMM conv kernels with a
-3x3 zero-padded filter (conv_px{,2,3}_kernel / conv_wgrad_*kernel with KH=3, RFL=0) plus the split-K
-reduction kernels dispatched right after each of them."""
+3x3 zero-padded filter (conv_px{,2,3}_kernel / conv_halo3_kernel / conv_wgrad_*kernel / conv_whalo_kernel
+with KH=3, RFL=0) plus the split-K / wgrad reduction kernels dispatched right after each of them."""
 import csv
 import json
 import os
@@ -37,6 +37,10 @@ def is_conv3(name):
         return a[7] == 3 and a[10] == 0
     if "conv_wgrad_stem_kernel" in name:   # <CIN>: the 7x7/2 stem
         return False
+    if "conv_halo3_kernel" in name:        # <MODE, NT, ITEMS, DBG, RFL, EXT>: stride-1 3x3
+        return (len(a) < 5 or a[4] == 0) and (len(a) < 6 or a[5] == 0)
+    if "conv_whalo_kernel" in name:        # <ITEMS, KS>: stride-1 3x3 zero-padded filter gradient
+        return True
     if "conv_wgrad_px3_kernel" in name:    # <BM, BN, WM, WN, KH, KW, S, RFL, CW, NT>
         return a[4] == 3 and a[7] == 0
     if "conv_wgrad16_kernel" in name:      # <MT, KH, KW, RFL>
@@ -47,7 +51,7 @@ def is_conv3(name):
 
 
 def is_reduce(name):
-    return "splitk_reduce" in name
+    return "splitk_reduce" in name or "wgrad_reduce" in name
 
 
 def read_csv(path):
