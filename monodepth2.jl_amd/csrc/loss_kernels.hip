@@ -93,12 +93,25 @@ __global__ __launch_bounds__(256) void disp_sum_kernel(DispSumBatch b) {
 // Edge-aware smoothness on the mean-normalised full-res disparity (src/utils.jl:163-177,
 // src/training.jl:64-67), forward + the local part of the backward.
 // ---------------------------------------------------------------------------------------------
-constexpr int SM_W = 64, SM_H = 4;
+// A wave owns 62 columns (lanes 1..62; lanes 0 and 63 hold the neighbouring columns x0-1 and
+// x0+62) and walks SM_R rows top to bottom (plus the row above its band) with the current and
+// the next row in registers: each pixel's disparity (the align-corners upsample) and image
+// values are formed ONCE, the right neighbour comes from lane + 1 and the left pair's weight from
+// lane - 1 by DPP, the row above's vertical weight from the previous step, the row two ahead is
+// loaded while the current one is computed.  4 waves = 4 stacked bands per block.  (The previous
+// LDS-tile form evaluated every disparity 2-3 times and every image value 4 times: 55-61 us per
+// launch at B=12.)  Same per-pixel arithmetic and evaluation order as before.
+constexpr int SM_TW = 62, SM_R = 8, SM_BR = 4 * SM_R;
+
+__device__ __forceinline__ float sm_from_left(float v) {    // lane i <- lane i-1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float sm_from_right(float v) {   // lane i <- lane i+1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
+}
 
 template <int C>
 __global__ __launch_bounds__(256) void smooth_kernel(SmoothBatch b) {
-  constexpr int EW = SM_W + 1, EH = SM_H + 1, NE = EW * EH;
-  __shared__ float s_ex[NE], s_ey[NE];
   __shared__ float s_red[4 * 3];
   __shared__ double s_redd[4];
   const int sc = blockIdx.z / b.s[0].N;       // scale; every scale shares N, W, H
@@ -106,7 +119,13 @@ __global__ __launch_bounds__(256) void smooth_kernel(SmoothBatch b) {
   const int W = a.W, H = a.H;
   const long HW = (long)W * H;
   const int n = blockIdx.z - sc * a.N;
-  const int x0 = blockIdx.x * SM_W, y0 = blockIdx.y * SM_H;
+  const int lane = threadIdx.x & 63, wq = threadIdx.x >> 6;
+  const int x = (int)blockIdx.x * SM_TW + lane - 1;
+  const int y0 = (int)blockIdx.y * SM_BR + wq * SM_R;
+  const bool colv = x >= 0 && x < W;
+  const bool own = colv && lane >= 1 && lane <= SM_TW;
+  const bool hpair = colv && x + 1 < W && lane < 63;   // the pair (x, x+1) exists
+  const int xc = min(max(x, 0), W - 1);
   const float* dsp = a.disp + (long)n * a.dw * a.dh;
   const float* img = a.img + (long)n * a.img_sample_stride;
   float inv = 1.f;                          // slow_depth: no mean normalisation
@@ -117,56 +136,63 @@ __global__ __launch_bounds__(256) void smooth_kernel(SmoothBatch b) {
   }
   const float cx = 1.f / ((float)a.N * (float)H * (float)(W - 1));
   const float cy = 1.f / ((float)a.N * (float)(H - 1) * (float)W);
-  float lx = 0.f, ly = 0.f;
-  for (int i = threadIdx.x; i < NE; i += 256) {
-    const int ex = i % EW, ey = i / EW;
-    const int gx = x0 - 1 + ex, gy = y0 - 1 + ey;
-    float vx = 0.f, vy = 0.f;
-    if (gx >= 0 && gx < W && gy >= 0 && gy < H) {
+  auto load_row = [&](int r, float& d, float (&im)[C]) {
+    const int rc = min(max(r, 0), H - 1);
+    d = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, xc, rc);
+#pragma unroll
+    for (int c = 0; c < C; ++c) im[c] = img[c * HW + (long)rc * W + xc];
+  };
+  float lx = 0.f, ly = 0.f, tsum = 0.f;
+  double tsumd = 0.0;
+  if (y0 < H) {                             // wave-uniform
+    const int r1 = min(y0 + SM_R, H);
+    float d0, i0[C], d1, i1[C], d2, i2[C];
+    load_row(y0 - 1, d0, i0);
+    load_row(y0, d1, i1);
+    float vyprev = 0.f;
+    for (int r = y0 - 1; r < r1; ++r) {     // wave-uniform trip count
+      load_row(r + 2, d2, i2);              // two rows ahead
       // differences are formed on the raw disparity and scaled afterwards: (d_q - d_r) * inv is
       // sign-exact (no FMA-contraction residue where d_q == d_r, abs'(0) = 0)
-      const float dq = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy);
-      const bool own = ex >= 1 && ey >= 1;
-      if (gx + 1 < W) {
-        const float dr = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx + 1, gy);
+      float vx = 0.f, vy = 0.f;
+      {
+        const float dr = sm_from_right(d0);
         float gi = 0.f;
 #pragma unroll
-        for (int c = 0; c < C; ++c)
-          gi += fabsf(img[c * HW + (long)gy * W + gx] - img[c * HW + (long)gy * W + gx + 1]);
+        for (int c = 0; c < C; ++c) gi += fabsf(i0[c] - sm_from_right(i0[c]));
         const float e = expf(-gi / (float)C) * cx;
-        const float df = (dq - dr) * inv;
-        vx = e * (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f));
-        if (own) lx += fabsf(df) * e;
+        const float df = (d0 - dr) * inv;
+        if (r >= 0 && hpair) {
+          vx = e * (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f));
+          if (own && r >= y0) lx += fabsf(df) * e;
+        }
       }
-      if (gy + 1 < H) {
-        const float dd = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy + 1);
+      if (r >= 0 && r + 1 < H && colv) {
         float gi = 0.f;
 #pragma unroll
-        for (int c = 0; c < C; ++c)
-          gi += fabsf(img[c * HW + (long)gy * W + gx] - img[c * HW + (long)(gy + 1) * W + gx]);
+        for (int c = 0; c < C; ++c) gi += fabsf(i0[c] - i1[c]);
         const float e = expf(-gi / (float)C) * cy;
-        const float df = (dq - dd) * inv;
+        const float df = (d0 - d1) * inv;
         vy = e * (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f));
-        if (own) ly += fabsf(df) * e;
+        if (own && r >= y0) ly += fabsf(df) * e;
+      }
+      const float vxl = sm_from_left(vx);
+      if (r >= y0 && own) {
+        const float u = vx - vxl + vy - vyprev;
+        const long q = ((long)n * H + r) * W + x;
+        a.g_disp[q] += a.ws * u * inv;
+        tsum += u * d0;
+        tsumd += (double)u * (double)d0;
+      }
+      vyprev = vy;
+      d0 = d1;
+      d1 = d2;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        i0[c] = i1[c];
+        i1[c] = i2[c];
       }
     }
-    s_ex[i] = vx;
-    s_ey[i] = vy;
-  }
-  __syncthreads();
-  float tsum = 0.f;
-  double tsumd = 0.0;
-  for (int i = threadIdx.x; i < SM_W * SM_H; i += 256) {
-    const int tx = i % SM_W, ty = i / SM_W;
-    const int gx = x0 + tx, gy = y0 + ty;
-    if (gx >= W || gy >= H) continue;
-    const int e = (ty + 1) * EW + (tx + 1);
-    const float u = s_ex[e] - s_ex[e - 1] + s_ey[e] - s_ey[e - EW];
-    const long q = ((long)n * H + gy) * W + gx;
-    a.g_disp[q] += a.ws * u * inv;
-    const float dv = disp_at(dsp, a.dw, a.dh, a.rx, a.ry, W, H, gx, gy);
-    tsum += u * dv;
-    tsumd += (double)u * (double)dv;
   }
   float v[3] = {lx + ly, tsum, 0.f};
   block_sum256<3>(v, s_red);
@@ -519,7 +545,7 @@ int launch_warp_vis(const PhotoArgs& a, int scale, const Geom& g, int C, float* 
   return MD2_OK;
 }
 
-long smooth_blocks(int W, int H, int N) { return (long)cdiv(W, SM_W) * cdiv(H, SM_H) * N; }
+long smooth_blocks(int W, int H, int N) { return (long)cdiv(W, SM_TW) * cdiv(H, SM_BR) * N; }
 
 int launch_disp_sum(const DispSumBatch& b, int nscales, hipStream_t st) {
   MD2_CHECK_ARG(nscales >= 1 && nscales <= MAX_SCALES, "disp_sum: nscales");
@@ -535,7 +561,7 @@ int launch_smooth(const SmoothArgs* a, int nscales, int C, hipStream_t st) {
     MD2_CHECK_ARG(a[k].N == a[0].N && a[k].W == a[0].W && a[k].H == a[0].H, "smooth: scales differ in N/W/H");
     b.s[k] = a[k];
   }
-  dim3 grid(cdiv(a[0].W, SM_W), cdiv(a[0].H, SM_H), a[0].N * nscales);
+  dim3 grid(cdiv(a[0].W, SM_TW), cdiv(a[0].H, SM_BR), a[0].N * nscales);
   if (C == 3)
     hipLaunchKernelGGL(smooth_kernel<3>, grid, dim3(256), 0, st, b);
   else if (C == 1)
