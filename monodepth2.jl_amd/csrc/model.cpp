@@ -268,6 +268,7 @@ class Model {
   // scratch
   float *DA = nullptr, *DY = nullptr, *G = nullptr, *DYD = nullptr;
   float *DPRE = nullptr, *DUP = nullptr, *DO1 = nullptr;
+  float *DPRE2 = nullptr, *DO1b = nullptr;   // second slots of the decoder's ping-pong (below)
   ConvWorkspace cws{};
   // Side stream for independent branches, each with its OWN scratch (split-K workspace,
   // bias-gradient partials, activation-pullback buffer, BN partials slot 1) so they can run
@@ -318,12 +319,20 @@ class Model {
     const char* v = getenv("MD2_DEC_WGRAD_STREAM");
     return !(v && v[0] == '0');
   }();
+  // (measured neutral: 6.114 vs 6.122 ms interleaved -- the model stream's waits there are the
+  // side's total share, not the buffer reuse; off by default, MD2_DEC_PINGPONG=1 with MD2_TUNING)
+  const bool dec_pingpong = tuning_knob("MD2_DEC_PINGPONG", 0) != 0;
   // DepthDecoder backward: each conv's filter gradient on the side stream beside its data
   // gradient and the rest of the branch (the decoder convs fill a fraction of the chip).  The
   // side reads DPRE / DO1 and the bias partials of the act_bias before it, so those buffers are
   // reused only after the side's event (bias partials double-buffered: bp_dec[0] for c2, [1] for c1)
+  // (MD2_DEC_PINGPONG=1) DPRE / DO1 / their bias partials alternate between two slots branch by
+  // branch, so the model stream reuses a buffer only after the side's filter gradient of the
+  // branch before the previous one
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c2 = nullptr, ev_c1 = nullptr;
+  hipEvent_t ev_c2b = nullptr, ev_c1b = nullptr;
   float* bp_dec[2] = {nullptr, nullptr};
+  float* bp_dec2[2] = {nullptr, nullptr};
   bool pose_overlap() const { return pose_stream && side && !prof; }
   bool wgrad_overlap() const { return dec_wgrad_stream && side && !prof; }
   bool down_overlap() const { return down_stream && side && !prof; }
@@ -339,6 +348,9 @@ class Model {
     return !(v && v[0] == '0');
   }();
   const int enc_wgrad_from = tuning_knob("MD2_ENC_WGRAD_FROM", 3);
+  // (1: -45 us per step, 6.555 vs 6.60 ms interleaved; the side stream was the longer path of the
+  // layer-4 segment)
+  const bool enc_wgrad_main0 = tuning_knob("MD2_ENC_WGRAD_MAIN0", 1) != 0;
   bool enc_overlap(int si) const { return enc_wgrad_stream && side && !prof && si >= enc_wgrad_from; }
   float* DY2 = nullptr;
   hipEvent_t ev_y[2] = {nullptr, nullptr};
@@ -380,7 +392,7 @@ class Model {
     if (seg_ev) (void)hipEventDestroy(seg_ev);
     if (upd_ev) (void)hipEventDestroy(upd_ev);
     if (fork_ev) (void)hipEventDestroy(fork_ev);
-    for (hipEvent_t e : {ev_a, ev_b, ev_c2, ev_c1, ev_y[0], ev_y[1]})
+    for (hipEvent_t e : {ev_a, ev_b, ev_c2, ev_c1, ev_c2b, ev_c1b, ev_y[0], ev_y[1]})
       if (e) (void)hipEventDestroy(e);
     if (join_ev) (void)hipEventDestroy(join_ev);
     if (g.st) (void)hipStreamDestroy(g.st);
@@ -632,6 +644,10 @@ class Model {
     MD2_TRY(alloc(&DPRE, scratch));
     MD2_TRY(alloc(&DUP, scratch));
     MD2_TRY(alloc(&DO1, scratch));
+    if (dec_pingpong) {
+      MD2_TRY(alloc(&DPRE2, scratch));
+      MD2_TRY(alloc(&DO1b, scratch));
+    }
     {
       float* q;
       MD2_TRY(alloc(&q, wsn / sizeof(float) + 64));
@@ -653,10 +669,12 @@ class Model {
     MD2_HIP(hipEventCreateWithFlags(&upd_ev, hipEventDisableTiming));
     MD2_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     MD2_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
-    for (hipEvent_t* e : {&ev_a, &ev_b, &ev_c2, &ev_c1, &ev_y[0], &ev_y[1]})
+    for (hipEvent_t* e : {&ev_a, &ev_b, &ev_c2, &ev_c1, &ev_c2b, &ev_c1b, &ev_y[0], &ev_y[1]})
       MD2_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     MD2_TRY(alloc(&bp_dec[0], BP_WS));
     MD2_TRY(alloc(&bp_dec[1], BP_WS));
+    MD2_TRY(alloc(&bp_dec2[0], BP_WS));
+    MD2_TRY(alloc(&bp_dec2[1], BP_WS));
     {
       double* q;
       void* v;
@@ -1354,7 +1372,10 @@ class Model {
       const int cin = e.conv.p.cin;
       const long hin = (long)e.conv.s.H * e.conv.s.W;
       float* dy = ybuf(ycur);
-      if (eov) {   // filter gradient beside the data gradient; dy untouched until ev_y[ycur]
+      // MD2_ENC_WGRAD_MAIN0=1 (tuning): the first conv's filter gradient of each block stays on
+      // the model stream, after its data gradient (balances the side stream's share)
+      const bool wmain = eov && k == 0 && enc_wgrad_main0;
+      if (eov && !wmain) {   // filter gradient beside the data gradient; dy untouched until ev_y[ycur]
         MD2_TRY(stream_wait(st, side, fork_ev));
         side_ws = true;
         const int rc = conv_w(e.conv, nimg, tin(xin, cin, hin), dy, side);
@@ -1362,7 +1383,7 @@ class Model {
         MD2_TRY(rc);
         MD2_HIP(hipEventRecord(ev_y[ycur], side));
         y_pending[ycur] = true;
-      } else {
+      } else if (!wmain) {
         MD2_TRY(conv_w(e.conv, nimg, tin(xin, cin, hin), dy, st));
       }
       if (k > 0) {
@@ -1374,6 +1395,7 @@ class Model {
       } else {
         if (dov) MD2_HIP(hipStreamWaitEvent(st, join_ev, 0));   // b.d_in written by the 1x1 dgrad
         MD2_TRY(conv_d(e.conv, nimg, dy, b.d_in, (long)cin * hin, 1, st));
+        if (wmain) MD2_TRY(conv_w(e.conv, nimg, tin(xin, cin, hin), dy, st));
       }
     }
     return MD2_OK;
@@ -1440,8 +1462,16 @@ class Model {
       DecBranch& d = br[i];
       const long hw = (long)d.h * d.w, hw2 = 4 * hw;
       const int co = d.b.cout;
-      if (wov && i < nb - 1) MD2_HIP(hipStreamWaitEvent(st, ev_c2, 0));   // DPRE, bp_dec[0] free
-      MD2_TRY(act_bias(d.o2, d.d_o2, DPRE, ND, co, hw2, ACT_ELU, st, wov ? bp_dec[0] : nullptr));
+      // ping-pong slot of this branch (MD2_DEC_PINGPONG=0: one slot, A/B)
+      const int slot = dec_pingpong ? ((nb - 1 - i) & 1) : 0;
+      const int lag = dec_pingpong ? 2 : 1;
+      float* const dpre = slot ? DPRE2 : DPRE;
+      float* const do1 = slot ? DO1b : DO1;
+      const hipEvent_t evc2 = slot ? ev_c2b : ev_c2, evc1 = slot ? ev_c1b : ev_c1;
+      float* const bpc2 = slot ? bp_dec2[0] : bp_dec[0];
+      float* const bpc1 = slot ? bp_dec2[1] : bp_dec[1];
+      if (wov && i < nb - lag) MD2_HIP(hipStreamWaitEvent(st, evc2, 0));   // dpre, bpc2 free
+      MD2_TRY(act_bias(d.o2, d.d_o2, dpre, ND, co, hw2, ACT_ELU, st, wov ? bpc2 : nullptr));
       TensorIn in = tin(d.up, co, hw2);
       float* dskip = nullptr;
       long skip_bs = 0;
@@ -1460,19 +1490,19 @@ class Model {
         }
       }
       if (wov) {
-        MD2_TRY(wgrad_side(d.c2, in, DPRE, ev_a, ev_c2));
-        MD2_TRY(conv_d(d.c2, ND, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
+        MD2_TRY(wgrad_side(d.c2, in, dpre, ev_a, evc2));
+        MD2_TRY(conv_d(d.c2, ND, dpre, DUP, co * hw2, 0, st, dskip, skip_bs, co));
       } else {
-        MD2_TRY(conv_wd(d.c2, ND, in, DPRE, DUP, co * hw2, 0, st, dskip, skip_bs, co));
+        MD2_TRY(conv_wd(d.c2, ND, in, dpre, DUP, co * hw2, 0, st, dskip, skip_bs, co));
       }
       if (E > 0 && d.b.cskip > 0) {
         // _repeat pullback: the skip gradient of the target features = sum over the planes
         const int fi = 4 - d.b.bid;
         MD2_TRY(plane_sum(d_emb[fi], N, NP, featC[fi] + Ep, featC[fi], hw2, d_skip[fi], 0, st));
       }
-      if (wov && i < nb - 1) MD2_HIP(hipStreamWaitEvent(st, ev_c1, 0));   // DO1, bp_dec[1] free
-      MD2_TRY(upsample2_bwd(DUP, ND, co, d.h, d.w, DO1, st));
-      MD2_TRY(act_bias(d.o1, DO1, DO1, ND, co, hw, ACT_ELU, st, wov ? bp_dec[1] : nullptr));
+      if (wov && i < nb - lag) MD2_HIP(hipStreamWaitEvent(st, evc1, 0));   // do1, bpc1 free
+      MD2_TRY(upsample2_bwd(DUP, ND, co, d.h, d.w, do1, st));
+      MD2_TRY(act_bias(d.o1, do1, do1, ND, co, hw, ACT_ELU, st, wov ? bpc1 : nullptr));
       const float* xin;
       int cin;
       float* dx;
@@ -1495,15 +1525,16 @@ class Model {
         acc = br[i - 1].head >= 0 ? 1 : 0;   // on top of the head's dx
       }
       if (wov) {
-        MD2_TRY(wgrad_side(d.c1, tin(xin, cin, hw), DO1, ev_b, ev_c1));
-        MD2_TRY(conv_d(d.c1, ND, DO1, dx, (long)cin * hw, acc, st));
+        MD2_TRY(wgrad_side(d.c1, tin(xin, cin, hw), do1, ev_b, evc1));
+        MD2_TRY(conv_d(d.c1, ND, do1, dx, (long)cin * hw, acc, st));
       } else {
-        MD2_TRY(conv_wd(d.c1, ND, tin(xin, cin, hw), DO1, dx, (long)cin * hw, acc, st));
+        MD2_TRY(conv_wd(d.c1, ND, tin(xin, cin, hw), do1, dx, (long)cin * hw, acc, st));
       }
       if (i == 0 && E > 0)
         MD2_TRY(plane_sum(d_emb[4], N, NP, cin, featC[4], hw, d_f4 + (long)T0 * featC[4] * hw, 1, st));
     }
-    if (wov) MD2_HIP(hipStreamWaitEvent(st, ev_c1, 0));   // every decoder filter gradient final
+    // every decoder filter gradient final: the side runs in order, so its last event covers all
+    if (wov) MD2_HIP(hipStreamWaitEvent(st, (dec_pingpong && ((nb - 1) & 1)) ? ev_c1b : ev_c1, 0));
     return MD2_OK;
   }
 
