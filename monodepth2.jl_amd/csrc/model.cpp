@@ -322,6 +322,10 @@ class Model {
   // (measured neutral: 6.114 vs 6.122 ms interleaved -- the model stream's waits there are the
   // side's total share, not the buffer reuse; off by default, MD2_DEC_PINGPONG=1 with MD2_TUNING)
   const bool dec_pingpong = tuning_knob("MD2_DEC_PINGPONG", 0) != 0;
+  // decoder filter gradients kept on the model stream (balance): bit i of MD2_DEC_WMAIN_C2 /
+  // MD2_DEC_WMAIN_C1 = branch i's c2 / c1 (branch nb-1 is the full-resolution one)
+  const int dec_wmain_c2 = tuning_knob("MD2_DEC_WMAIN_C2", 0);
+  const int dec_wmain_c1 = tuning_knob("MD2_DEC_WMAIN_C1", 0);
   // DepthDecoder backward: each conv's filter gradient on the side stream beside its data
   // gradient and the rest of the branch (the decoder convs fill a fraction of the chip).  The
   // side reads DPRE / DO1 and the bias partials of the act_bias before it, so those buffers are
@@ -1489,7 +1493,7 @@ class Model {
           skip_bs = (long)featC[fi] * hw2;
         }
       }
-      if (wov) {
+      if (wov && !((dec_wmain_c2 >> i) & 1)) {
         MD2_TRY(wgrad_side(d.c2, in, dpre, ev_a, evc2));
         MD2_TRY(conv_d(d.c2, ND, dpre, DUP, co * hw2, 0, st, dskip, skip_bs, co));
       } else {
@@ -1524,7 +1528,7 @@ class Model {
         dx = br[i - 1].d_o2;
         acc = br[i - 1].head >= 0 ? 1 : 0;   // on top of the head's dx
       }
-      if (wov) {
+      if (wov && !((dec_wmain_c1 >> i) & 1)) {
         MD2_TRY(wgrad_side(d.c1, tin(xin, cin, hw), do1, ev_b, evc1));
         MD2_TRY(conv_d(d.c1, ND, do1, dx, (long)cin * hw, acc, st));
       } else {
