@@ -60,6 +60,27 @@ def test_fused_splitk_bn_bitwise(B, H, W, switch):
         assert torch.equal(of.m, ou.m) and torch.equal(of.v, ou.v), i
 
 
+@pytest.mark.parametrize("B,H,W", [(12, 128, 416), (2, 64, 128)])
+def test_fused_bnstats_close(B, H, W):
+    """BatchNorm statistics from the LDS-halo forward's epilogue (per-tile fp64 partials,
+    MD2_FUSE_BNSTATS) against the separate statistics pass: the same fp64 sums in another order,
+    so mean / invstd agree to an ulp, not bitwise.  Losses within 1e-6 relative at every step;
+    parameters within ADAM's per-step bound (lr per step: an update can flip where a gradient
+    component sits at the rounding level)."""
+    import md2hip.dist
+    xs = [D.triplets(B, 3, H, W, seed=s).float().cuda().contiguous() for s in (5, 6, 7)]
+    mf, exf, of = _setup(True, H, W, B, "MD2_FUSE_BNSTATS")
+    mu, exu, ou = _setup(False, H, W, B, "MD2_FUSE_BNSTATS")
+    comm = md2hip.dist.GradAllReduce(force=False)
+    for i, x in enumerate(xs):
+        lf = md2hip.dist.train_step(exf, mf, of, x, comm).clone()
+        lu = md2hip.dist.train_step(exu, mu, ou, x, comm).clone()
+        torch.cuda.synchronize()
+        assert abs(float(lf) - float(lu)) <= 1e-6 * abs(float(lu)), (i, float(lf), float(lu))
+        dp = (mf.flat - mu.flat).abs().max().item()
+        assert dp <= 2.0 * 1e-4 * (i + 1) + 1e-7, (i, dp)
+
+
 _KNOB_CHILD = r"""
 import os, sys
 root, out = sys.argv[1], sys.argv[2]
