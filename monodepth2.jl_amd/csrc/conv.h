@@ -54,6 +54,13 @@ struct TensorOut {
 struct SplitKDefer {
   const float* slab = nullptr;
   int splits = 0;
+  // BatchNorm statistics from the conv epilogue (conv_fwd only): the caller offers a partials
+  // buffer [Cout][>= ceil(N*Ho*Wo / 256)][2] (fp64 sum, sum of squares); when the conv runs the
+  // LDS-halo kernel without split-K it writes one partial per 256-pixel tile and sets
+  // stats_parts to the tile count (0: not written, run bn_stats_partial as usual)
+  double* stats = nullptr;
+  int stats_parts = 0;
+  bool keep_reduce = false;   // input: never defer the split-K reduction (only the statistics)
 };
 
 struct ConvWorkspace {

@@ -382,7 +382,8 @@ class Model {
     return MD2_OK;
   }
   BNStatsWs bnws{};
-  long bn_slot = 0;       // doubles per partials slot (slot 1: the downsample BN of a block)
+  long bn_slot = 0;
+  double* bn_collapsed = nullptr;   // [2 slots][4096 channels][2]: collapsed epilogue partials       // doubles per partials slot (slot 1: the downsample BN of a block)
   void* tail_ws = nullptr;
   LossTailCfg tail{};
   float* loss_buf = nullptr;
@@ -485,6 +486,7 @@ class Model {
     auto track = [&](long n) { scratch = std::max(scratch, (size_t)n); };
     auto bnws_need = [&](int Cc, long HW) {
       bnmax = std::max(bnmax, (long)Cc * bn_parts(Cc, B, HW) * 2);
+      bnmax = std::max(bnmax, (long)Cc * ((B * HW + 255) / 256) * 2);   // per-tile epilogue partials
     };
     // ---- encoder
     MD2_TRY(make_conv(stem, spec.stem, cfg.H, cfg.W, false, wsn));
@@ -687,6 +689,9 @@ class Model {
       allocs.push_back(v);
       q = (double*)v;
       bnws.partials = q;
+      MD2_HIP(hipMalloc(&v, 2 * 4096 * 2 * sizeof(double)));
+      allocs.push_back(v);
+      bn_collapsed = (double*)v;
     }
     // ---- loss tail (src/training.jl:21-78).  MPI mode: the ND plane disparities are the batch
     // (training.jl:42-51 reshapes depth to (1, W*H, dn) with dn = num_bins*N); the poses and the
@@ -804,8 +809,30 @@ class Model {
     o.bs0 = out_bs;
     o.bias = P(c.p.b);
     SplitKDefer d;
+    // the LDS-halo forward without split-K takes the statistics in its epilogue (MD2_FUSE_BNSTATS=0:
+    // the separate bn_stats_partial pass; within 1 ulp of mean / invstd, not bit-identical: the
+    // fp64 sums run in another order)
+    BNStatsWs wst = bn_ws(bn, nimg, HW, slot);
+    if (fuse_bnstats) d.stats = wst.partials;
+    d.keep_reduce = !fuse_splitk;
     hipEvent_t e = prof_begin(st);
-    MD2_TRY(conv_fwd(s, in, c.wpf, o, ws_conv(), st, fuse_splitk ? &d : nullptr));
+    MD2_TRY(conv_fwd(s, in, c.wpf, o, ws_conv(), st, fuse_splitk || fuse_bnstats ? &d : nullptr));
+    if (d.stats_parts > 0) {
+      // (the apply passes finalise the tile partials per block, behind their own loads;
+      // MD2_BN_COLLAPSE=1: one collapse launch first -- measured slower, 6 us per launch)
+      if (bn_collapse) {
+        MD2_CHECK_ARG(bn.p.c <= 4096, "conv_f_bn: BN channels");
+        double* col = bn_collapsed + (long)slot * 2 * 4096;
+        MD2_TRY(bn_partials_collapse(wst.partials, bn.p.c, d.stats_parts, col, st));
+        bn.part = col;
+        bn.parts = 1;
+      } else {
+        bn.part = wst.partials;
+        bn.parts = d.stats_parts;
+      }
+      prof_end(e, c.cat, conv_flops(s), st, "fwd", &s);
+      return MD2_OK;
+    }
     if (d.splits > 0) {
       BNStatsWs w = bn_ws(bn, nimg, HW, slot);
       MD2_TRY(bn_stats_partial_slabs(SlabIn{d.slab, d.splits}, y, nimg, bn.p.c, HW, w, st));
@@ -829,6 +856,12 @@ class Model {
   // bit-identity test)
   const bool fuse_pool_bwd = [] {
     const char* v = getenv("MD2_FUSE_POOL_BWD");
+    return !(v && v[0] == '0');
+  }();
+  const bool bn_collapse = tuning_knob("MD2_BN_COLLAPSE", 0) != 0;
+  // MD2_FUSE_BNSTATS=0 restores the statistics pass after the LDS-halo forward convs
+  const bool fuse_bnstats = [] {
+    const char* v = getenv("MD2_FUSE_BNSTATS");
     return !(v && v[0] == '0');
   }();
   // MD2_FUSE_SPLITK=0 restores the separate reduction launches (A/B measurement)

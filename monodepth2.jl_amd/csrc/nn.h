@@ -61,6 +61,9 @@ struct BNApplyFused {
   int relu = 0;
 };
 int bn_stats_partial(const float* y, int N, int C, long HW, BNStatsWs ws, hipStream_t st);
+// [C][parts][2] statistics partials -> [C][1][2] (fixed order per channel), so the apply passes'
+// per-block finalise reads one partial instead of `parts` (the conv epilogue's per-tile partials)
+int bn_partials_collapse(const double* part, int C, int parts, double* out, hipStream_t st);
 int bn_stats_partial_slabs(SlabIn sl, float* y, int N, int C, long HW, BNStatsWs ws, hipStream_t st);
 int bn_apply_fused(const BNApplyFused& p, float* out, int N, int C, long HW, hipStream_t st);
 // backward reduce: g = dout * (mask_out > 0 if mask_out) ; dgamma = sum g*xhat, dbeta = sum g

@@ -123,6 +123,30 @@ __global__ void bn_stats_final_kernel(const double* __restrict__ part, int C, in
   }
 }
 
+__global__ __launch_bounds__(64) void bn_partials_collapse_kernel(const double* __restrict__ part, int parts,
+                                                                  double* __restrict__ out) {
+  const int c = blockIdx.x;
+  double a = 0.0, aa = 0.0;
+  const double* q = part + (long)c * parts * 2;
+  for (int p = threadIdx.x; p < parts; p += 64) {
+    a += q[2 * p];
+    aa += q[2 * p + 1];
+  }
+  a = wave_sum_d(a);
+  aa = wave_sum_d(aa);
+  if (threadIdx.x == 0) {
+    out[2 * c] = a;
+    out[2 * c + 1] = aa;
+  }
+}
+
+int bn_partials_collapse(const double* part, int C, int parts, double* out, hipStream_t st) {
+  MD2_CHECK_ARG(part && out && C >= 1 && parts >= 1, "bn_partials_collapse: arguments");
+  hipLaunchKernelGGL(bn_partials_collapse_kernel, dim3(C), dim3(64), 0, st, part, parts, out);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 int bn_stats_partial(const float* y, int N, int C, long HW, BNStatsWs ws, hipStream_t st) {
   MD2_TRY(check_u31((long)N * C * HW));
   MD2_CHECK_ARG(ws.parts >= 1 && ws.parts <= N, "bn_stats: parts must split the images");
@@ -288,6 +312,20 @@ __global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNApplyFused p, flo
   const uint32_t u0 = blockIdx.x * (256u * UPT);
   const uint32_t pl0 = fdiv(u0, fdU);
   const uint32_t npl = fdiv(min(u0 + 256u * UPT - 1u, nu - 1u), fdU) - pl0 + 1u;
+  // the block's loads are issued before the per-plane finalise (independent of it): its partial
+  // sums -- up to one per 256-pixel tile when the conv epilogue took the statistics -- are read
+  // while the tensor's bytes are in flight
+  float4 v[UPT], q2[UPT], qr[UPT];
+  if (VEC) {
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const uint32_t u = u0 + threadIdx.x + 256u * j;
+      const long i = 4L * (u < nu ? u : 0u);
+      v[j] = *reinterpret_cast<const float4*>(p.y + i);
+      if (p.y2) q2[j] = *reinterpret_cast<const float4*>(p.y2 + i);
+      if (p.res) qr[j] = *reinterpret_cast<const float4*>(p.res + i);
+    }
+  }
   for (uint32_t t = threadIdx.x >> 6; t < npl; t += 4) {   // wave-uniform plane loop
     const uint32_t pl = pl0 + t;
     const int c = (int)(pl - fdiv(pl, fdC) * fdC.d);
@@ -305,16 +343,6 @@ __global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNApplyFused p, flo
   }
   __syncthreads();
   if (VEC) {
-    // every load of the thread's UPT units in flight before the first is used
-    float4 v[UPT], q2[UPT], qr[UPT];
-#pragma unroll
-    for (int j = 0; j < UPT; ++j) {
-      const uint32_t u = u0 + threadIdx.x + 256u * j;
-      const long i = 4L * (u < nu ? u : 0u);
-      v[j] = *reinterpret_cast<const float4*>(p.y + i);
-      if (p.y2) q2[j] = *reinterpret_cast<const float4*>(p.y2 + i);
-      if (p.res) qr[j] = *reinterpret_cast<const float4*>(p.res + i);
-    }
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
       const uint32_t u = u0 + threadIdx.x + 256u * j;
