@@ -128,3 +128,32 @@ def test_tuning_knobs_ignored_without_md2_tuning(tmp_path):
         res[name] = np.load(out)
     assert np.array_equal(res["clean"], res["knobs"])
     assert not np.array_equal(res["clean"], res["tuned"])
+
+
+# round-5 placement / regrouping switches: each regroups the same arithmetic (other streams, other
+# buffers, another loop order with the same per-output fma chain), so the step must not move a bit
+BITWISE_TUNING = {"MD2_ENC_WGRAD_MAIN0": "0", "MD2_DEC_PINGPONG": "1", "MD2_HEAD_ROWS": "1"}
+
+
+@pytest.mark.timeout(420)
+def test_bitwise_tuning_switches(tmp_path):
+    """MD2_ENC_WGRAD_MAIN0=0 (every layer-4 filter gradient on the side stream), MD2_DEC_PINGPONG=1
+    (two-slot decoder pullback buffers), MD2_HEAD_ROWS=1 (row-walking heads forward): two train
+    steps at B=2 64x128 give parameters bit-identical to the defaults."""
+    import subprocess
+    import sys
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = {k: v for k, v in os.environ.items() if not k.startswith("MD2_")}
+    runs = {"clean": base}
+    for k, v in BITWISE_TUNING.items():
+        runs[k] = dict(base, MD2_TUNING="1", **{k: v})
+    res = {}
+    for name, env in runs.items():
+        out = str(tmp_path / f"{name}.npy")
+        r = subprocess.run([sys.executable, "-c", _KNOB_CHILD, root, out], env=env, capture_output=True,
+                           text=True, timeout=200)
+        assert r.returncode == 0, (name, r.stderr[-3000:])
+        res[name] = np.load(out)
+    for k in BITWISE_TUNING:
+        assert np.array_equal(res["clean"], res[k]), k
