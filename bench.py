@@ -77,14 +77,50 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _kfd_gpus(root=KFD_NODES) -> int:
+    """GPU agents in the KFD topology (nodes whose properties report SIMDs), -1 if unreadable --
+    read from sysfs, so no HIP runtime is loaded."""
+    try:
+        names = os.listdir(root)
+    except OSError:
+        return -1
+    n = 0
+    for d in names:
+        try:
+            with open(os.path.join(root, d, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+    return n
+
+
 def _visible_devices(selftest: bool) -> int:
-    """GPUs this process can see, counted WITHOUT initialising HIP (torch.cuda.device_count does
-    not on this image), so the parent may still start the ranks.  The launcher self-test takes
-    MD2_BENCH_FAKE_DEVICES instead (CPU-only containers)."""
+    """GPUs this process can see, counted WITHOUT initialising HIP, so that the parent may still
+    start the ranks: the KFD topology in sysfs, capped by HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.  -1 when the topology is unreadable (no fallback
+    to a HIP device query).  The launcher self-test takes MD2_BENCH_FAKE_DEVICES instead
+    (CPU-only containers)."""
     if selftest and "MD2_BENCH_FAKE_DEVICES" in os.environ:
         return int(os.environ["MD2_BENCH_FAKE_DEVICES"])
-    import torch
-    return torch.cuda.device_count()
+    n = _kfd_gpus()
+    if n < 0:
+        return -1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip()]))
+    return n
+
+
+def _under_profiler() -> bool:
+    """rocprofv3 initialises the GPU in every process it wraps (its preloaded tool library), so a
+    launcher parent under it would spawn ranks from a GPU-initialised process."""
+    return any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
 
 
 def launch_local(args) -> int:
@@ -92,9 +128,19 @@ def launch_local(args) -> int:
     MASTER_ADDR=127.0.0.1 / MASTER_PORT, as torch.distributed.run sets them) and wait for all of
     them.  Rank 0 prints the JSON line on the inherited stdout.  A rank that fails ends the others
     (their exact PIDs) and its exit status is returned."""
+    import signal
     import subprocess
     n = args.gpus
+    if _under_profiler() and not args.launcher_selftest:
+        print("bench.py: --gpus N > 1 under a profiler: the profiler initialises the GPU in this "
+              "parent; launch the ranks with `python -m torch.distributed.run` from a clean shell",
+              file=sys.stderr, flush=True)
+        return 2
     have = _visible_devices(args.launcher_selftest)
+    if have < 0:
+        print("bench.py: cannot count GPUs without initialising HIP (no KFD topology in sysfs); "
+              "launch the ranks with `python -m torch.distributed.run`", file=sys.stderr, flush=True)
+        return 2
     if have < n:
         print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}; refusing to run "
               f"fewer ranks", file=sys.stderr, flush=True)
@@ -107,23 +153,44 @@ def launch_local(args) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     print(f"bench.py: started {n} ranks (pids {[p.pid for p in procs]}), master 127.0.0.1:{port}",
           file=sys.stderr, flush=True)
+    def stop(live, grace=10.0):
+        for q in live:
+            if q.poll() is None:
+                q.terminate()
+        t_end = time.time() + grace
+        for q in live:
+            try:
+                q.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+
+    # a SIGTERM / SIGINT to the launcher (a driver's timeout) ends the ranks it started -- their
+    # exact PIDs -- instead of orphaning them on the GPUs and the rendezvous port
+    def on_signal(signum, frame):
+        print(f"bench.py: signal {signum}: stopping ranks {[p.pid for p in procs]}", file=sys.stderr, flush=True)
+        stop(procs)
+        sys.exit(128 + signum)
+
+    old_handlers = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
     live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 128 - code
-                print(f"bench.py: rank pid {p.pid} exited with {code}; stopping the others",
-                      file=sys.stderr, flush=True)
-                for q in live:
-                    q.terminate()
-        time.sleep(0.05)
-    for p in procs:
-        p.wait()
+    try:
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank pid {p.pid} exited with {code}; stopping the others",
+                          file=sys.stderr, flush=True)
+                    stop(live)
+            time.sleep(0.05)
+    finally:
+        stop(procs)
+        for sig, h in old_handlers.items():
+            signal.signal(sig, h)
     return rc
 
 
@@ -270,6 +337,18 @@ def pmc_traffic():
     return round(t["bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
+def pmc_mfma_busy():
+    """MFMA pipe busy fraction of the roofline set (per family and overall) from the newest
+    committed profile carrying it (tools/profile_round.sh's SQ_VALU_MFMA_BUSY_CYCLES pass)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+        with open(path) as f:
+            m = json.load(f).get("mfma_busy")
+        if m:
+            return m, os.path.relpath(path, ROOT)
+    return None, None
+
+
 def pmc_photo_traffic(batch):
     """HBM bytes per launch of the photometric kernel at this batch from the newest committed
     tools/pmc_photo.sh profile (profiles/r*_pmc_photo.json; FETCH doubled per the gfx950 note,
@@ -398,8 +477,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     c1 = comm_counts()
-    if comm is None:
-        comm_info = None
+    if comm is None or not dp:
+        comm_info = None            # single GPU: no transport, no all-reduce
     elif isinstance(comm, md2hip.comm.Comm):
         comm_info = {"transport": "md2_comm (RCCL, library-owned)", "nranks": comm.query()[1]}
     else:
@@ -467,11 +546,16 @@ def main():
             # the committed PMC profiles are of the default workload (ResNet-18, B=12, 416x128)
             default = (args.arch, B, H, W) == (18, 12, 128, 416)
             traffic, tsrc = pmc_traffic() if default else (None, None)
+            busy, bsrc = pmc_mfma_busy() if default else (None, None)
             out["roofline"] = {"bound": "mfma", "kernel": "implicit-GEMM zero-padded 3x3 convs (encoder+pose): fwd+dgrad conv_halo3 (LDS halo, stride 1) / conv_px3 (stride 2), wgrad conv_whalo (LDS halo, layers 2-4 + pose) / conv_wgrad_px3 (bf16x6 split products, fp32 sums), + split-K / wgrad reduce",
                                "achieved": round(ach, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
                                "peak_note": "peak = fp32 MFMA (the reference's arithmetic, algorithmic fp32 FLOPs); "
-                                            f"the bf16x6 kernels' own ceiling is {PEAK_BF16X6_TFLOPS:.1f} TFLOP/s",
+                                            f"the bf16x6 kernels issue 6 bf16 MFMAs per fp32 product: their own "
+                                            f"ceiling is {PEAK_BF16X6_TFLOPS:.1f} TFLOP/s (frac_issued)",
+                               "peak_issued": round(PEAK_BF16X6_TFLOPS, 1),
+                               "frac_issued": round(ach / PEAK_BF16X6_TFLOPS, 4),
+                               "mfma_busy": busy, "mfma_busy_source": bsrc,
                                "traffic_source": tsrc,
                                "launches": n, "algorithmic_flop_per_step": flop, "kernel_ms_per_step": round(ms, 4),
                                "probe": f"median of {args.probe_steps} profiled steps; fastest step "

@@ -39,6 +39,9 @@ extern "C" {
 #define MD2_ESTATE 5
 
 int md2_abi_version(void);
+/* hash of the sources the library was built from (csrc/Makefile BUILD_ID): bindings recompute it
+ * from their source tree and refuse a stale library */
+const char* md2_build_id(void);
 /* thread-local message of the last failing call (never NULL). */
 const char* md2_last_error(void);
 /* number of visible HIP devices (host call; does not initialise a context). */
@@ -345,6 +348,24 @@ int md2_model_forward_loss(md2_model* m, const float* x, const float* auto_loss,
                            float* terms, void* stream);
 /* backward in segments (0 = pose+depth decoders, 1..4 = layer4..layer1, 5 = stem); after
  * segment k the flat gradient range [off, off+len) is final (bucket for the DP all-reduce) */
+/* (m)(x, source_ids, target_id) -> (disparities, poses) (src/model.jl:31-55; called at
+ * src/training.jl:26 and, bare, scripts/script.jl:93): the forward only -- encoder, DepthDecoder,
+ * PoseDecoder, no loss tail.  disp[level] ([batch*num_bins][h][w]) and *pose ([2*batch][6]) are
+ * set to the model's output buffers (either may be NULL), the values md2_model_forward_loss would
+ * produce for the same x, bit for bit.  A backward after it needs the outputs' cotangents. */
+int md2_model_forward(md2_model* m, const float* x, const float** disp, const float** pose,
+                      void* stream);
+/* The pullback of md2_model_forward from caller cotangents (a host that differentiates its own
+ * loss, e.g. the reference's train_loss through Zygote): d_disp[level] = d L / d disparity of that
+ * level, laid out as the outputs (NULL array or entry: zero), d_pose [2*batch][6] (NULL: zero).
+ * md2_model_set_cotangents only installs them -- the backward segments then run as after
+ * md2_model_forward_loss (DP buckets unchanged); md2_model_backward_from installs them and runs
+ * every segment.  The flat gradient equals the fused path's bit for bit when the cotangents equal
+ * the loss tail's own (md2_loss_fwd_bwd with sigmoid_grad = 0). */
+int md2_model_set_cotangents(md2_model* m, const float* const* d_disp, const float* d_pose,
+                             void* stream);
+int md2_model_backward_from(md2_model* m, const float* const* d_disp, const float* d_pose,
+                            void* stream);
 int md2_model_num_segments(md2_model* m);
 int md2_model_backward_segment(md2_model* m, int k, long long* off, long long* len,
                                void* stream);

@@ -167,8 +167,98 @@ function outputs(m::HIPModel)
                 (Ptr{Cvoid}, Ptr{Ptr{Float32}}, Ptr{Cint}, Ptr{Cint}, Ref{Ptr{Float32}}),
                 m.handle, d, w, h, pose))
     n = m.cfg.batch
-    disps = [unsafe_wrap(ROCArray, d[k], (Int(w[k]), Int(h[k]), 1, n)) for k in 1:m.cfg.n_levels]
+    np = m.cfg.embedding_levels > 0 ? Int(m.cfg.num_bins) : 1          # MPI: plane images
+    disps = [unsafe_wrap(ROCArray, d[k], (Int(w[k]), Int(h[k]), 1, n * np)) for k in 1:m.cfg.n_levels]
     return disps, unsafe_wrap(ROCArray, pose[], (6, 2n))
+end
+
+"""
+    HIPModel(model, cache, params; num_bins=32)
+
+The HIP model of a reference `Model(encoder, depth_decoder, pose_decoder)` (src/model.jl:24-29,
+built as in scripts/script.jl:77-81) for one `TrainCache` / `Params`: the architecture (ResNet
+depth, input channels, `scale_levels`, `embedding_levels`) is read off the Flux model and its
+parameters are copied (conv kernels flipped into the library layout) into the flat θ.
+"""
+function HIPModel(model, cache, params; num_bins=32)
+    enc, dec = model.encoder, model.depth_decoder
+    ch = collect(enc.stages)
+    levels = cumsum([length(b) for b in dec.branches])
+    emb = size(dec.branches[1][1].c1.d.weight, 3) - ch[end]
+    ps = collect(Flux.params(model))
+    in_ch = size(ps[1], 3)                         # the stem conv (kw,kh,cin,64)
+    for arch in (ch[end] == 2048 ? (50,) : (18, 34))
+        cfg = ModelCfg(arch, in_ch, levels, params, cache; embedding_levels=emb,
+                       num_bins=emb > 0 ? num_bins : 1)
+        param_count(cfg)[1] == length(ps) || continue
+        return HIPModel(cfg, flat_params(cfg, ps))
+    end
+    error("HIPModel: the Flux model matches no ResidualNetwork(18/34/50) + DepthDecoder + PoseDecoder table")
+end
+
+"""
+    (m::HIPModel)(x, source_ids, target_id) -> (disparities, poses)
+
+`(m::Model)(x, source_ids, target_id)` of src/model.jl:31-55 (called by train_loss at
+src/training.jl:26 and bare at scripts/script.jl:93) on the HIP path, forward only: `disparities`
+one (w,h,1,n) array per scale level ((w,h,1,n*num_bins) in MPI mode), `poses` one
+`(rvec = (3,n), tvec = (3,1,n))` per source (the fields train_loss reads of `Pose`).  The rrule's
+pullback runs the library's backward from the caller's cotangents (md2_model_backward_from), so
+the reference's own train_loss can be differentiated through it by Zygote.  `source_ids` /
+`target_id` must be the ones the model was built with.
+"""
+function (m::HIPModel)(x::ROCArray{Float32,5}, source_ids, target_id)
+    (target_id - 1, source_ids[1] - 1, source_ids[2] - 1) == (m.cfg.target, m.cfg.src0, m.cfg.src1) ||
+        error("HIPModel: target_id / source_ids differ from the config the model was built with")
+    _forward(m, m.θ, x)
+end
+
+function _forward(m::HIPModel, θ::ROCVector{Float32}, x::ROCArray{Float32,5})
+    θ === m.θ || error("HIPModel: θ must be the model's own parameter vector")
+    m.packed || repack!(m)
+    check(ccall((:md2_model_forward, lib), Cint,
+                (Ptr{Cvoid}, Ptr{Float32}, Ptr{Ptr{Float32}}, Ptr{Ptr{Float32}}, Ptr{Cvoid}),
+                m.handle, x, C_NULL, C_NULL, stream_ptr()))
+    disps, pose = outputs(m)
+    n = m.cfg.batch
+    poses = [(rvec = pose[1:3, (s - 1) * n + 1:s * n], tvec = reshape(pose[4:6, (s - 1) * n + 1:s * n], 3, 1, n))
+             for s in 1:2]
+    return [copy(d) for d in disps], poses        # copies: the next forward reuses the buffers
+end
+
+function ChainRulesCore.rrule(::typeof(_forward), m::HIPModel, θ::ROCVector{Float32}, x)
+    y = _forward(m, θ, x)
+    function forward_pullback(Δ)
+        Δd, Δp = unthunk(Δ[1]), unthunk(Δ[2])
+        keep = Any[]
+        dptrs = fill(Ptr{Float32}(C_NULL), 5)
+        if !(Δd isa AbstractZero)
+            for (k, d) in enumerate(Δd)
+                d = unthunk(d)
+                d isa AbstractZero && continue
+                a = ROCArray{Float32}(d); push!(keep, a); dptrs[k] = pointer(a)
+            end
+        end
+        dpose = Ptr{Float32}(C_NULL)
+        if !(Δp isa AbstractZero)
+            n = m.cfg.batch; P = fill!(ROCArray{Float32}(undef, 6, 2n), 0f0)
+            for (s, p) in enumerate(Δp)
+                p = unthunk(p)
+                p isa AbstractZero && continue
+                r, t = unthunk(p.rvec), unthunk(p.tvec)
+                r isa AbstractZero || (P[1:3, (s - 1) * n + 1:s * n] .= reshape(r, 3, n))
+                t isa AbstractZero || (P[4:6, (s - 1) * n + 1:s * n] .= reshape(t, 3, n))
+            end
+            push!(keep, P); dpose = pointer(P)
+        end
+        check(ccall((:md2_model_backward_from, lib), Cint,
+                    (Ptr{Cvoid}, Ptr{Ptr{Float32}}, Ptr{Float32}, Ptr{Cvoid}),
+                    m.handle, dptrs, dpose, stream_ptr()))
+        AMDGPU.synchronize()                 # the cotangent copies in `keep` are read asynchronously
+        m.packed = false
+        return NoTangent(), NoTangent(), copy(m.∇θ), NoTangent()
+    end
+    return y, forward_pullback
 end
 
 # the loss-tail config of this model (for the visualisation pass)

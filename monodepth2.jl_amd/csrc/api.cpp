@@ -116,6 +116,7 @@ int tuning_knob(const char* name, int dflt) {
 extern "C" {
 
 int md2_abi_version(void) { return MD2_ABI_VERSION; }
+const char* md2_build_id(void) { return MD2_BUILD_ID; }
 
 const char* md2_last_error(void) { return md2::last_error(); }
 
@@ -454,6 +455,28 @@ int md2_model_forward_loss(md2_model* m, const float* x, const float* auto_loss,
                            float* terms, void* stream) {
   MD2_CHECK_ARG(m, "model");
   return model_forward_loss(m->impl, x, auto_loss, loss, terms, (hipStream_t)stream);
+}
+
+int md2_model_forward(md2_model* m, const float* x, const float** disp, const float** pose,
+                      void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  MD2_TRY(model_forward(m->impl, x, (hipStream_t)stream));
+  return model_outputs(m->impl, disp, nullptr, nullptr, pose);
+}
+
+int md2_model_set_cotangents(md2_model* m, const float* const* d_disp, const float* d_pose,
+                             void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  return model_set_cotangents(m->impl, d_disp, d_pose, (hipStream_t)stream);
+}
+
+int md2_model_backward_from(md2_model* m, const float* const* d_disp, const float* d_pose,
+                            void* stream) {
+  MD2_CHECK_ARG(m, "model");
+  MD2_TRY(model_set_cotangents(m->impl, d_disp, d_pose, (hipStream_t)stream));
+  for (int k = 0; k < model_num_segments(m->impl); ++k)
+    MD2_TRY(model_backward_segment(m->impl, k, nullptr, nullptr, (hipStream_t)stream));
+  return MD2_OK;
 }
 
 int md2_model_num_segments(md2_model* m) { return m ? model_num_segments(m->impl) : 0; }

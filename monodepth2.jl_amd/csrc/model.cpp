@@ -382,8 +382,8 @@ class Model {
     return MD2_OK;
   }
   BNStatsWs bnws{};
-  long bn_slot = 0;
-  double* bn_collapsed = nullptr;   // [2 slots][4096 channels][2]: collapsed epilogue partials       // doubles per partials slot (slot 1: the downsample BN of a block)
+  long bn_slot = 0;                 // doubles per partials slot (slot 1: the downsample BN of a block)
+  double* bn_collapsed = nullptr;   // [2 slots][4096 channels][2]: collapsed epilogue partials
   void* tail_ws = nullptr;
   LossTailCfg tail{};
   float* loss_buf = nullptr;
@@ -1166,8 +1166,9 @@ class Model {
     return pose_head_fwd(pc2, 2 * N, 256, hw4, P(spec.p3.w), P(spec.p3.b), means, pose, st);
   }
 
-  int forward_loss(const float* x, const float* automask, float* loss, float* terms,
-                   hipStream_t st) {
+  // (m)(x, source_ids, target_id) (src/model.jl:31-55): encoder on the 3N frames, DepthDecoder on
+  // the targets, PoseDecoder on the pairs -- disparities and poses, no loss tail
+  int forward(const float* x, hipStream_t st) {
     const long fs = (long)cfg.arch.in_ch * cfg.H * cfg.W;
     TensorIn in;
     in.p0 = x;
@@ -1185,6 +1186,12 @@ class Model {
       MD2_TRY(decoder_fwd(N, T0, st));
       MD2_TRY(pose_fwd(st));
     }
+    return MD2_OK;
+  }
+
+  int forward_loss(const float* x, const float* automask, float* loss, float* terms,
+                   hipStream_t st) {
+    MD2_TRY(forward(x, st));
     const float* disps[MAX_SCALES] = {};
     LossTailOut o{};
     int li = 0;
@@ -1613,7 +1620,24 @@ class Model {
     return conv_w(stem, B, in, DY, st);
   }
 
+  // caller cotangents (d disp per level, d pose) of a forward-only call: the head pullback and
+  // the pose gradient buffers the backward segments read, as the fused loss tail writes them
+  int set_cotangents(const float* const* d_disp, const float* d_pose_in, hipStream_t st) {
+    int li = 0;
+    for (auto& d : br)
+      if (d.head >= 0) {
+        MD2_TRY(sigmoid_cotangent(d_disp ? d_disp[li] : nullptr, d.disp, d.d_head, (long)ND * 4 * d.h * d.w, st));
+        ++li;
+      }
+    if (d_pose_in) MD2_HIP(hipMemcpyAsync(d_pose, d_pose_in, sizeof(float) * 12 * N, hipMemcpyDefault, st));
+    else MD2_HIP(hipMemsetAsync(d_pose, 0, sizeof(float) * 12 * N, st));
+    return MD2_OK;
+  }
+
   const float* cur_x = nullptr;
+  // 0: the last forward was forward-only (the backward needs md2_model_set_cotangents first);
+  // 1: the backward's cotangents are in place (forward_loss, or set_cotangents after forward)
+  int cot_ready = 0;
   std::string dbg_name;   // storage behind model_debug_tensor's name
 };
 
@@ -1677,7 +1701,27 @@ int model_forward_loss(Model* m, const float* x, const float* automask, float* l
   MD2_CHECK_ARG(m && x, "model/x");
   MD2_TRY(m->adam_join(st));   // pending per-segment updates (model_adam_segment)
   m->cur_x = x;
+  m->cot_ready = 1;
   return m->forward_loss(x, automask, loss, terms, st);
+}
+
+int model_forward(Model* m, const float* x, hipStream_t st) {
+  MD2_CHECK_ARG(m && x, "model/x");
+  MD2_TRY(m->adam_join(st));   // pending per-segment updates (model_adam_segment)
+  m->cur_x = x;
+  m->cot_ready = 0;
+  return m->forward(x, st);
+}
+
+int model_set_cotangents(Model* m, const float* const* d_disp, const float* d_pose, hipStream_t st) {
+  MD2_CHECK_ARG(m, "model");
+  if (!m->cur_x) {
+    set_error("set_cotangents: no pending forward (none yet, or eval_disparity ran since)");
+    return MD2_ESTATE;
+  }
+  MD2_TRY(m->set_cotangents(d_disp, d_pose, st));
+  m->cot_ready = 1;
+  return MD2_OK;
 }
 
 int model_num_segments(Model* m) { return m ? 6 : 0; }
@@ -1709,6 +1753,7 @@ static int capture_step(Model* m, bool with_auto, float* adam_m, float* adam_v, 
   MD2_HIP(hipStreamBeginCapture(g.st, hipStreamCaptureModeThreadLocal));
   auto body = [&]() -> int {
     m->cur_x = g.x;
+    m->cot_ready = 1;
     MD2_TRY(m->forward_loss(g.x, with_auto ? g.autoloss : nullptr, g.loss, nullptr, g.st));
     for (int k = 0; k < model_num_segments(m); ++k) MD2_TRY(model_backward_segment(m, k, nullptr, nullptr, g.st));
     MD2_TRY(adam_prep(g.step, g.bc, 0.9f, 0.999f, g.st));
@@ -1759,6 +1804,7 @@ int model_train_step_graph(Model* m, const float* x, const float* auto_loss, flo
   MD2_HIP(hipGraphLaunch(g.exec, st));
   MD2_HIP(hipMemcpyAsync(loss, g.loss, sizeof(float), hipMemcpyDeviceToDevice, st));
   m->cur_x = g.x;
+  m->cot_ready = 1;
   g.next_step = step + 1;
   return MD2_OK;
 }
@@ -1769,6 +1815,10 @@ int model_backward_segment(Model* m, int k, long* off, long* len, hipStream_t st
   MD2_CHECK_ARG(m, "model");
   if (!m->cur_x) {
     set_error("backward_segment: no pending forward_loss (none yet, or eval_disparity ran since)");
+    return MD2_ESTATE;
+  }
+  if (!m->cot_ready) {
+    set_error("backward_segment: forward-only call without cotangents (md2_model_set_cotangents)");
     return MD2_ESTATE;
   }
   MD2_CHECK_ARG(k >= 0 && k < 6, "segment index");
@@ -1985,7 +2035,7 @@ int model_get_grads_flux(Model* m, float* flux, hipStream_t st) {
 // train_loss pullback with an upstream cotangent: the fused loss tail formed d loss / d (disp,
 // pose) for dloss = 1 during the forward; scale them before backward segment 0
 int model_scale_loss_cotangent(Model* m, float dloss, hipStream_t st) {
-  MD2_CHECK_ARG(m && m->cur_x, "loss cotangent before forward");
+  MD2_CHECK_ARG(m && m->cur_x && m->cot_ready, "loss cotangent before forward_loss");
   if (dloss == 1.f) return MD2_OK;
   for (auto& d : m->br)
     if (d.head >= 0) MD2_TRY(scale_inplace(d.d_head, (long)m->ND * 4 * d.h * d.w, dloss, st));

@@ -59,6 +59,12 @@ void model_destroy(Model* m);
 // train path
 int model_forward_loss(Model* m, const float* x, const float* automask, float* loss, float* terms,
                        hipStream_t st);
+// forward only ((m)(x, source_ids, target_id), src/model.jl:31-55): outputs via model_outputs;
+// a backward after it needs model_set_cotangents
+int model_forward(Model* m, const float* x, hipStream_t st);
+// cotangents of the last forward's outputs: d_disp[level] w.r.t. each disparity (nullptr array or
+// entry: zero), d_pose [2N][6] (nullptr: zero); then model_backward_segment as after forward_loss
+int model_set_cotangents(Model* m, const float* const* d_disp, const float* d_pose, hipStream_t st);
 int model_num_segments(Model* m);
 // runs backward segment k (0 = pose+decoder ... last = stem); [off, off+len) of the flat gradient
 // is final afterwards

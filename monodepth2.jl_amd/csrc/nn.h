@@ -139,6 +139,8 @@ int pair_grad_gather(const float* dpin, int N, int C, long HW, const int a[2], c
 
 // ---- Flux ADAM over the flat parameter vector ----
 int scale_inplace(float* x, long n, float s, hipStream_t st);
+// out = g .* (s .* (1 - s)) (g == nullptr: 0), the sigmoid head's pullback
+int sigmoid_cotangent(const float* g, const float* s, float* out, long n, hipStream_t st);
 // [planes][kh][kw] with both spatial axes reversed (Flux true-convolution <-> cross-correlation)
 int flip_taps(const float* src, float* dst, long planes, int kh, int kw, hipStream_t st);
 // graph-replayable ADAM: *step += 1 and bc = (1 - b1^t, 1 - b2^t) on the device, then the update

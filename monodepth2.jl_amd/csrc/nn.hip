@@ -1622,6 +1622,25 @@ int scale_inplace(float* x, long n, float s, hipStream_t st) {
   return MD2_OK;
 }
 
+// d pre = d disp .* (s .* (1 - s)) -- the sigmoid head's pullback of a caller cotangent on the
+// disparity (md2_model_set_cotangents); the same rounding as the loss tail's fused form
+// (loss_kernels.hip up_adjoint: acc *= sg * (1 - sg)), so a cotangent that equals the loss tail's
+// own d disp gives a bit-identical head gradient.  g == nullptr: zero cotangent.
+__global__ __launch_bounds__(256) void sigmoid_cot_kernel(const float* __restrict__ g,
+                                                          const float* __restrict__ s,
+                                                          float* __restrict__ out, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float sg = s[i];
+  out[i] = g ? g[i] * (sg * (1.f - sg)) : 0.f;
+}
+int sigmoid_cotangent(const float* g, const float* s, float* out, long n, hipStream_t st) {
+  if (n <= 0) return MD2_OK;
+  hipLaunchKernelGGL(sigmoid_cot_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, g, s, out, n);
+  MD2_LAUNCH_CHECK();
+  return MD2_OK;
+}
+
 // Flux Conv weights (kw,kh,cin,cout) = C-order [cout][cin][kh][kw] of a TRUE convolution ->
 // the library's cross-correlation layout (and back: the map is an involution): both spatial axes
 // reversed, dst[o][i][y][x] = src[o][i][kh-1-y][kw-1-x]

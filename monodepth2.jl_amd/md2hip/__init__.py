@@ -7,7 +7,7 @@ op runs the HIP kernels and a missing library raises."""
 from ._lib import MD2Error, lib  # noqa: F401
 from .loss import Params, TrainCache, depth10k_intrinsics, loss_tail, pack_poses  # noqa: F401
 from .model import (ADAM, DepthDecoder, Model, Pose, PoseDecoder, ResidualNetwork, ResNet,  # noqa: F401
-                    disparity_bins, eval_disparity, flux_params, gradient, param_table, set_flux_params,
+                    disparity_bins, eval_disparity, flux_params, gradient, param_table, pullback, set_flux_params,
                     train_loss, train_step)
 from .slow_depth import SlowDepth, adam_update, slow_depth  # noqa: F401
 from .checkpoint import load_checkpoint, save_checkpoint  # noqa: F401
@@ -16,7 +16,7 @@ from .mpi import MPIDepthDecoder, mpi_forward  # noqa: F401
 
 __all__ = ["Params", "TrainCache", "depth10k_intrinsics", "loss_tail", "pack_poses", "lib", "MD2Error",
            "ADAM", "DepthDecoder", "Model", "Pose", "PoseDecoder", "ResidualNetwork", "ResNet",
-           "disparity_bins", "eval_disparity", "flux_params", "gradient", "param_table", "set_flux_params", "train_loss",
+           "disparity_bins", "eval_disparity", "flux_params", "gradient", "param_table", "pullback", "set_flux_params", "train_loss",
            "train_step",
            "SlowDepth", "adam_update", "slow_depth", "load_checkpoint", "save_checkpoint",
            "DataLoader", "DChain", "Depth10k", "FlipX", "KittyDataset", "find_static",

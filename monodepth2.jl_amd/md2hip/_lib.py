@@ -75,12 +75,31 @@ class WarpCfg(C.Structure):
 _lib = None
 _load_error = None
 
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+INCLUDE_H = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "md2.h")
+
+
+def source_build_id():
+    """The hash csrc/Makefile embeds as md2_build_id(): sha256 of the sorted csrc sources
+    (*.hip *.cpp *.h *.inc), the Makefile and include/md2.h, concatenated; None without a tree."""
+    import hashlib
+    if not os.path.isdir(CSRC):
+        return None
+    names = sorted(set(n for n in os.listdir(CSRC)
+                       if os.path.splitext(n)[1] in (".hip", ".cpp", ".h", ".inc")))
+    h = hashlib.sha256()
+    for path in [os.path.join(CSRC, n) for n in names] + [os.path.join(CSRC, "Makefile"), INCLUDE_H]:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
 P = C.c_void_p
 FP = C.POINTER(C.c_void_p)
 
 _SIGS = {
     "md2_abi_version": (C.c_int, []),
     "md2_last_error": (C.c_char_p, []),
+    "md2_build_id": (C.c_char_p, []),
     "md2_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "md2_memcpy_d2d": (C.c_int, [P, P, C.c_size_t, P]),
     "md2_loss_workspace_size": (C.c_size_t, [C.POINTER(LossCfg)]),
@@ -106,6 +125,9 @@ _SIGS = {
     "md2_model_device_bytes": (C.c_size_t, [P]),
     "md2_model_repack": (C.c_int, [P, P]),
     "md2_model_forward_loss": (C.c_int, [P, P, P, P, P, P]),
+    "md2_model_forward": (C.c_int, [P, P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), P]),
+    "md2_model_set_cotangents": (C.c_int, [P, FP, P, P]),
+    "md2_model_backward_from": (C.c_int, [P, FP, P, P]),
     "md2_model_num_segments": (C.c_int, [P]),
     "md2_model_backward_segment": (C.c_int, [P, C.c_int, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong), P]),
     "md2_model_adam": (C.c_int, [P, P, P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_float, P]),
@@ -183,6 +205,11 @@ def lib():
     if got != ABI_VERSION:
         raise RuntimeError(f"{LIB_PATH} has ABI version {got}, this binding expects {ABI_VERSION}: "
                            "rebuild the library or update md2hip")
+    built = l.md2_build_id().decode()
+    want = source_build_id()
+    if want is not None and built != want and os.environ.get("MD2HIP_LIB") is None:
+        raise RuntimeError(f"{LIB_PATH} was built from other sources (build id {built}, tree {want}): "
+                           "stale library -- rebuild with `make -C monodepth2.jl_amd/csrc`")
     _lib = l
     return l
 

@@ -227,6 +227,32 @@ class _Executor:
         self.forwarded = self.pending = True
         return loss
 
+    def forward(self, x):
+        """``(m)(x, source_ids, target_id)`` alone (md2_model_forward): encoder, DepthDecoder and
+        PoseDecoder, no loss tail.  A backward after it needs ``set_cotangents``."""
+        self.sync()
+        check(lib().md2_model_forward(self.handle, ptr(x), None, None, stream_of(x.device)),
+              "md2_model_forward")
+        self.forwarded = self.pending = True
+        self.cotangents = False
+
+    def set_cotangents(self, d_disps=None, d_pose=None):
+        """The cotangents of the last forward's outputs (md2_model_set_cotangents): d_disps[l] like
+        the level-l disparities (None: zero), d_pose like the [2N, 6] poses (None: zero)."""
+        import torch
+        keep = []
+        arr = (C.c_void_p * 5)()
+        for i, d in enumerate(d_disps or []):
+            if d is not None:
+                d = d.to(self.model.device, torch.float32).contiguous()
+                keep.append(d)
+                arr[i] = d.data_ptr()
+        dp = None if d_pose is None else d_pose.to(self.model.device, torch.float32).contiguous()
+        check(lib().md2_model_set_cotangents(self.handle, arr, ptr(dp), stream_of(self.model.device)),
+              "md2_model_set_cotangents")
+        self._cot_keep = (keep, dp)           # the copies are async: keep the sources alive
+        self.cotangents = True
+
     def train_step_graph(self, x, opt: "ADAM", auto_loss=None, loss=None):
         """One full step (forward, loss, backward, Flux ADAM with opt's state) replayed as a
         captured hipGraph (md2_model_train_step_graph): the same kernels in the same order as
@@ -395,7 +421,7 @@ class Model:
         ex = self.executor(tuple(x.shape), cache, params, num_bins)
         if ex.emb:
             ex.set_bins(disparity_bins(N, num_bins, device=self.device) if bins is None else bins)
-        ex.forward_loss(x, None)
+        ex.forward(x)                       # forward only (md2_model_forward): no loss tail
         disps, pose = ex.outputs()
         return disps, [Pose(pose[s * N:(s + 1) * N, 0:3], pose[s * N:(s + 1) * N, 3:6]) for s in range(2)]
 
@@ -455,6 +481,24 @@ def gradient(model: Model, dloss: float = 1.0):
     if dloss != 1.0:
         check(lib().md2_model_loss_cotangent(ex.handle, float(dloss), stream_of(model.device)),
               "md2_model_loss_cotangent")
+    ex.backward()
+    return model.grad
+
+
+def pullback(model: Model, d_disps=None, d_poses=None):
+    """The pullback of the last ``model(x, source_ids, target_id)`` call from caller cotangents --
+    what Zygote runs when the caller differentiates its own loss of (disparities, poses): fills and
+    returns ``model.grad``.  ``d_disps[l]`` like the level-l disparities [N*num_bins, 1, h, w]
+    (None: zero); ``d_poses`` [Pose-like (d_rvec [N, 3], d_tvec [N, 3]) per source] or a [2N, 6]
+    tensor (None: zero).  The backward segments are the fused path's (md2_model_set_cotangents)."""
+    import torch
+    ex = model._last
+    if ex is None or not ex.forwarded:
+        raise RuntimeError("pullback() needs a preceding model(x, source_ids, target_id) call")
+    dp = d_poses
+    if d_poses is not None and not torch.is_tensor(d_poses):
+        dp = torch.cat([torch.cat([torch.as_tensor(r), torch.as_tensor(t)], 1) for r, t in d_poses], 0)
+    ex.set_cotangents(d_disps, dp)
     ex.backward()
     return model.grad
 

@@ -315,9 +315,11 @@ def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_i
 # forward deviation):
 #   forward     disparities per scale, poses: within max(1e-6, 2 x the fp32 floor);
 #               loss within max(1e-6, 4 x floor);
-#   end to end  every parameter tensor within max(1e-3, 4 x its fp32 floor) -- 1e-3 because no
-#               fp32 evaluation meets less on the encoder's BN gradients (cancelling sums; both
-#               fp32 realisations reach ~1e-3 there at B=12 416x128);
+#   end to end  every parameter tensor within max(2e-5, 4 x its fp32 floor) -- the floor is the
+#               max over four fp32 realisations, so the encoder's BN gradients (cancelling sums,
+#               ~1e-3 in every fp32 realisation at B=12 416x128) are held by their own floors and
+#               no tensor gets an absolute allowance far above its floor (all
+#               1,868 round-5 tensor checks passed at this bound);
 #   backward    (at the GPU's own forward point) within max(4 x floor_b, 4 x coherent, 2e-5; 1e-4
 #               for the Cout=1 heads' bias gradients) and never above max(1e-4, 2 x floor_b,
 #               1.25 x coherent).
@@ -328,7 +330,7 @@ def oracle_bounds(g, o=None, arch=18, levels=(2, 3, 4, 5), target_id=2, source_i
 # 640x192 their coherent sensitivity (1.6e-4, profiles/r04_parity_r50.json) exceeds the absolute
 # 1e-4.  The backward ceiling admits 1.25 x coherent for those tensors and nothing more.
 CEIL_BWD, CEIL_BWD_FLOOR, CEIL_BWD_COHERENT = 1e-4, 2.0, 1.25
-E2E_ABS, E2E_FLOOR = 1e-3, 4.0
+E2E_ABS, E2E_FLOOR = 2e-5, 4.0
 FWD_ABS, FWD_FLOOR = 1e-6, 2.0
 
 
@@ -357,7 +359,7 @@ def check_step(g, o, errs, b, label=""):
         warp-constant sensitivity, 2e-5; 1e-4 for the cancelling head biases) -- the GPU reproduces
         the exact gradient at its own forward point -- and never above max(1e-4, 2 x floor_b,
         1.25 x coherent);
-      * END TO END, per tensor: |gpu - oracle| within max(1e-3, 4 x the fp32 floor).
+      * END TO END, per tensor: |gpu - oracle| within max(2e-5, 4 x the fp32 floor).
     Every tensor's (err, bound, floors, explained, coherent) is written to parity_record_path(label)
     before anything is asserted."""
     floor = b["floor"]

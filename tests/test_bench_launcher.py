@@ -50,10 +50,37 @@ def test_too_few_devices_exits_nonzero():
 
 
 def test_real_device_count_is_checked():
-    # no fake count: this container has no GPU, so --gpus 2 must refuse (as on a 1-GPU box)
+    # no fake count: this container has no GPU (and no KFD topology), so --gpus 2 must refuse --
+    # either for too few devices (a 1-GPU box) or because they cannot be counted without HIP
     r = _run(["--gpus", "2"])
     assert r.returncode != 0
-    assert "needs 2 visible GPUs" in r.stderr
+    assert "needs 2 visible GPUs" in r.stderr or "cannot count GPUs without initialising HIP" in r.stderr
+
+
+def test_kfd_count_and_visible_device_cap(tmp_path, monkeypatch):
+    """The launcher counts GPU agents in the KFD sysfs topology (CPU nodes report no SIMDs) and
+    caps the count by the *_VISIBLE_DEVICES lists -- no HIP call in the parent."""
+    import bench
+    for i, simds in enumerate([0, 1024, 1024, 1024]):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count {0 if simds else 64}\nsimd_count {simds}\n")
+    monkeypatch.setattr(bench, "KFD_NODES", str(tmp_path))
+    assert bench._kfd_gpus(str(tmp_path)) == 3
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setattr(bench, "_kfd_gpus", lambda root=None: 3)
+    assert bench._visible_devices(False) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,2")
+    assert bench._visible_devices(False) == 2
+    monkeypatch.setattr(bench, "_kfd_gpus", lambda root=None: -1)
+    assert bench._visible_devices(False) == -1
+    assert bench._kfd_gpus(str(tmp_path / "missing")) == -1
+
+
+def test_launcher_refuses_under_profiler():
+    r = _run(["--gpus", "2"], {"ROCPROF_OUTPUT_PATH": "/tmp/x", "MD2_BENCH_FAKE_DEVICES": "2"})
+    assert r.returncode == 2 and "under a profiler" in r.stderr
 
 
 def test_under_a_launcher_does_not_spawn_again():

@@ -84,6 +84,46 @@ def dur(r):
     return int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
 
 
+def conv3_family(name):
+    """fwd / dgrad / wgrad and kernel of a roofline-set launch (None outside the set)."""
+    if not is_conv3(name):
+        return None
+    a = targs(name)
+    if "conv_halo3_kernel" in name:
+        return ("fwd" if a[0] == 0 else "dgrad") + " halo3"
+    if "conv_whalo_kernel" in name:
+        return "wgrad whalo"
+    if "conv_px3_kernel" in name or "conv_px2_kernel" in name:
+        return ("fwd" if a[0] == 0 else "dgrad") + " px3 (stride 2)"
+    return "wgrad px3"
+
+
+def mfma_busy(path):
+    """MFMA pipe busy fraction of the roofline set per family, from one --pmc pass of
+    SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE: busy / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
+    summed over the family's dispatches (tools/pmc_report.py's formula)."""
+    if not os.path.exists(path):
+        return None
+    per = defaultdict(lambda: defaultdict(float))
+    names = {}
+    for r in read_csv(path):
+        i = int(r["Dispatch_Id"])
+        per[i][r["Counter_Name"]] += float(r["Counter_Value"])
+        names[i] = r["Kernel_Name"]
+    fam = defaultdict(lambda: [0.0, 0.0, 0.0, 0])
+    for i, c in per.items():
+        f = conv3_family(names[i])
+        if f is None or "GRBM_GUI_ACTIVE" not in c:
+            continue
+        for key in (f, "set"):
+            fam[key][0] += c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+            fam[key][1] += c["GRBM_GUI_ACTIVE"] / 8 * 1024
+            fam[key][2] += c.get("SQ_INSTS_MFMA", 0.0)
+            fam[key][3] += 1
+    return {k: {"busy": round(v[0] / v[1], 4) if v[1] else None, "mfma_insts": v[2], "dispatches": v[3]}
+            for k, v in sorted(fam.items())}
+
+
 def main(src, tag):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -145,8 +185,9 @@ def main(src, tag):
                    "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports 1/2 of wide-read "
                            "bytes); these kernels mix 4-B gathers and 16-B loads, so the absolute is "
                            "uncalibrated; ratios between rounds are exact"}
+    mfma = mfma_busy(os.path.join(src, "mfma", "run_counter_collection.csv"))
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
-        json.dump({"counters": pmc, "traffic": traffic}, f, indent=1)
+        json.dump({"counters": pmc, "traffic": traffic, "mfma_busy": mfma}, f, indent=1)
 
     lines = [f"# Profile {tag}: bench.py on 1x MI355X (rocprofv3 --kernel-trace --stats)", ""]
     if bench:

@@ -14,4 +14,6 @@ timeout -k 10 300 python3 $BENCH > "$OUT/bench_plain.json"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $BENCH --no-probe > "$OUT/bench_trace.json"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 $BENCH --no-probe > "$OUT/bench_fetch.json"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 $BENCH --no-probe > "$OUT/bench_write.json"
+# MFMA pipe occupancy of every kernel (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
+timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_BUSY_CYCLES -d "$OUT/mfma" -o run --output-format csv -- python3 $BENCH --no-probe > "$OUT/bench_mfma.json"
 echo "profile done: $OUT"
