@@ -126,6 +126,9 @@ struct FinalizeArgs {
 
 // all a.nscales scales in one launch (photo.hip)
 int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st);
+// the packed-fp32 photometric kernel (photo2.hip), launched by launch_photometric
+int launch_photo2(const PhotoArgs& a, const Geom& g, const PhotoTiling& tl, int C, bool cells, long blocks,
+                  hipStream_t st);
 // identity-reprojection loss (training.jl:9-11): out [N][H][W] = min over the two raw sources of
 // photometric_loss(source, target)
 int launch_automask(const float* x, long x_sample_stride, long x_frame_stride, int target,

@@ -582,6 +582,10 @@ int launch_photometric(const PhotoArgs& a, const Geom& g, int C, hipStream_t st)
       return MD2_EINVAL;
     }
   }
+  // the packed-fp32 form (photo2.hip, bit-identical); MD2_PHOTO_V1=1 (read per launch, for the
+  // A/B and the bit-identity test) runs this file's scalar kernel
+  const char* v1 = std::getenv("MD2_PHOTO_V1");
+  if (!(v1 && v1[0] == '1')) return launch_photo2(a, g, tl, C, cells, blocks, st);
   const dim3 grid((unsigned)blocks), block(64);
   if (C == 3 && !cells)
     hipLaunchKernelGGL((photo_stream_kernel<3, false>), grid, block, 0, st, a, g, tl);

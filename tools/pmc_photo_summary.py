@@ -17,7 +17,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEY = "photo"
 W, H, C, NSCALES = 416, 128, 3, 4
-VALU_CYCLES = 2           # wave64 VALU instruction on gfx950 (SIMD-32), MI355X_MICROARCH.md
+VALU_CYCLES = 4           # wave64 f32 VALU issue on gfx950, measured (tools/micro/valu_rate.hip, profiles/r04_valu_rate.txt)
 SIMDS = 256 * 4
 
 
