@@ -721,97 +721,6 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(HeadBatch hb) {
     heads_fwd_body<2>(hb, hb.j[k], t, s_part);
 }
 
-// Row-walking forward (MD2_HEAD_ROWS, tuning): a block owns 62 pixel vectors of one image's rows
-// [r0, r0 + R) (lanes 0 / 63: the neighbouring vectors, for the DPP column taps), wave q sums
-// channel quarter q as in heads_fwd_body, but walks the rows with a 3-row register window: each
-// input row is loaded once per (channel, band) + 2 halo rows, instead of 3 times.  Same
-// per-output fma order and the same wave combine: bit-identical to heads_fwd_kernel (step digests
-// equal at B=12 and B=2).  Measured no faster in the train step (6.466 vs 6.444 ms interleaved:
-// the 3x row reloads of the tile kernel hit L2), so it stays opt-in.
-template <int R>
-__device__ void heads_fwd_rows_body(const HeadBatch& hb, const HeadJob& J, long t, float (*s_part)[64][4]) {
-  constexpr int V = 4;
-  const int lane = threadIdx.x & 63, wq = threadIdx.x >> 6;
-  const int Wv = J.W / V;
-  const int ncb = (Wv + HB_TILE - 1) / HB_TILE, nband = (J.H + R - 1) / R;
-  const int cb = (int)(t % ncb);
-  const long t2 = t / ncb;
-  const int band = (int)(t2 % nband), b = (int)(t2 / nband);
-  const int cx = cb * HB_TILE + lane - 1;
-  const bool own = lane >= 1 && lane <= HB_TILE && cx >= 0 && cx < Wv;
-  const int cxc = cx < 0 ? 0 : (cx >= Wv ? Wv - 1 : cx);
-  const int r0 = band * R, nr = min(R, J.H - r0);
-  const long HW = (long)J.H * J.W;
-  const float* xb = J.x.p + img_off(J.x, b);
-  const int cpw = (J.Cin + 3) >> 2;
-  const int cbg = wq * cpw, ce = min(J.Cin, cbg + cpw);
-  float out[R][V];
-#pragma unroll
-  for (int rr = 0; rr < R; ++rr)
-#pragma unroll
-    for (int i = 0; i < V; ++i) out[rr][i] = 0.f;
-  for (int c = cbg; c < ce; ++c) {
-    const float* xc = xb + c * HW;
-    float wt[9];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) wt[q] = J.wf.p[(long)c * J.wf.sc + (long)q * J.wf.st];
-    float a0[V + 2], a1[V + 2], a2[V + 2];
-    hb_row_reflect<V>(xc, hb_reflect(r0 - 1, J.H), J.W, cxc, Wv, a0);
-    hb_row_reflect<V>(xc, r0, J.W, cxc, Wv, a1);
-#pragma unroll
-    for (int rr = 0; rr < R; ++rr) {
-      if (rr >= nr) break;                            // wave-uniform
-      hb_row_reflect<V>(xc, hb_reflect(r0 + rr + 1, J.H), J.W, cxc, Wv, a2);
-#pragma unroll
-      for (int i = 0; i < V; ++i) {
-        float v = out[rr][i];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          v = fmaf(wt[q], a0[i + q], v);
-          v = fmaf(wt[3 + q], a1[i + q], v);
-          v = fmaf(wt[6 + q], a2[i + q], v);
-        }
-        out[rr][i] = v;
-      }
-#pragma unroll
-      for (int i = 0; i < V + 2; ++i) {
-        a0[i] = a1[i];
-        a1[i] = a2[i];
-      }
-    }
-  }
-  // wave combine in wave order through LDS, one row of the band at a time
-  const float bb = J.bias ? J.bias[0] : 0.f;
-#pragma unroll
-  for (int rr = 0; rr < R; ++rr) {
-    if (rr >= nr) break;                              // block-uniform
-    if (wq > 0) {
-#pragma unroll
-      for (int i = 0; i < V; ++i) s_part[wq - 1][lane][i] = out[rr][i];
-    }
-    __syncthreads();
-    if (wq == 0 && own) {
-      float y[V];
-#pragma unroll
-      for (int i = 0; i < V; ++i)
-        y[i] = act_f(((out[rr][i] + s_part[0][lane][i]) + s_part[1][lane][i]) + s_part[2][lane][i] + bb, hb.act);
-      vstore<V>(J.y + (long)b * J.ybs + (long)(r0 + rr) * J.W + cx * V, y);
-    }
-    __syncthreads();
-  }
-}
-
-// blocks of head k: [g0[k], g0[k + 1]); R = 8 rows per band (4 on maps under 64 rows)
-__global__ __launch_bounds__(256) void heads_fwd_rows_kernel(HeadBatch hb, const long* __restrict__ g0_unused) {
-  __shared__ float s_part[3][64][4];
-  const int k = hb_find(hb.f0, hb.n, blockIdx.x);
-  const long t = blockIdx.x - hb.f0[k];
-  if (hb.j[k].H >= 64)
-    heads_fwd_rows_body<8>(hb, hb.j[k], t, s_part);
-  else
-    heads_fwd_rows_body<4>(hb, hb.j[k], t, s_part);
-}
-
 // E(row) of the data gradient for pixel i at the three column taps kx (p.x = q.x + 1 - kx), from
 // the zero-padded row a (a[i+1] = column of pixel i), with the reflect folds in x: q = 1 also
 // takes p = 0 through kx = 0, q = W-2 takes p = W-1 through kx = 2
@@ -1181,23 +1090,6 @@ int heads_fwd(const HeadJob* jobs, int n, int act, hipStream_t st) {
   for (int k = 0; k < n; ++k) MD2_CHECK_ARG(jobs[k].y && jobs[k].wf.p, "heads_fwd: output / weights");
   HeadBatch hb = make_batch(jobs, n);
   hb.act = act;
-  static const int rows = tuning_knob("MD2_HEAD_ROWS", 0);
-  bool all4 = true;
-  for (int k = 0; k < n; ++k) all4 = all4 && hb.V[k] == 4;
-  if (rows && all4) {
-    // the row-walking forward: blocks per head = images x bands x column blocks (f0 re-used)
-    long f = 0;
-    for (int k = 0; k < n; ++k) {
-      const HeadJob& j = jobs[k];
-      const int R = j.H >= 64 ? 8 : 4;
-      hb.f0[k] = f;
-      f += (long)j.N * cdiv(j.H, R) * cdiv(j.W / 4, HB_TILE);
-    }
-    hb.f0[n] = f;
-    hipLaunchKernelGGL(heads_fwd_rows_kernel, dim3((unsigned)f), dim3(256), 0, st, hb, (const long*)nullptr);
-    MD2_LAUNCH_CHECK();
-    return MD2_OK;
-  }
   hipLaunchKernelGGL(heads_fwd_kernel, dim3((unsigned)hb.f0[n]), dim3(256), 0, st, hb);
   MD2_LAUNCH_CHECK();
   return MD2_OK;

@@ -268,7 +268,6 @@ class Model {
   // scratch
   float *DA = nullptr, *DY = nullptr, *G = nullptr, *DYD = nullptr;
   float *DPRE = nullptr, *DUP = nullptr, *DO1 = nullptr;
-  float *DPRE2 = nullptr, *DO1b = nullptr;   // second slots of the decoder's ping-pong (below)
   ConvWorkspace cws{};
   // Side stream for independent branches, each with its OWN scratch (split-K workspace,
   // bias-gradient partials, activation-pullback buffer, BN partials slot 1) so they can run
@@ -319,24 +318,12 @@ class Model {
     const char* v = getenv("MD2_DEC_WGRAD_STREAM");
     return !(v && v[0] == '0');
   }();
-  // (measured neutral: 6.114 vs 6.122 ms interleaved -- the model stream's waits there are the
-  // side's total share, not the buffer reuse; off by default, MD2_DEC_PINGPONG=1 with MD2_TUNING)
-  const bool dec_pingpong = tuning_knob("MD2_DEC_PINGPONG", 0) != 0;
-  // decoder filter gradients kept on the model stream (balance): bit i of MD2_DEC_WMAIN_C2 /
-  // MD2_DEC_WMAIN_C1 = branch i's c2 / c1 (branch nb-1 is the full-resolution one)
-  const int dec_wmain_c2 = tuning_knob("MD2_DEC_WMAIN_C2", 0);
-  const int dec_wmain_c1 = tuning_knob("MD2_DEC_WMAIN_C1", 0);
   // DepthDecoder backward: each conv's filter gradient on the side stream beside its data
   // gradient and the rest of the branch (the decoder convs fill a fraction of the chip).  The
   // side reads DPRE / DO1 and the bias partials of the act_bias before it, so those buffers are
   // reused only after the side's event (bias partials double-buffered: bp_dec[0] for c2, [1] for c1)
-  // (MD2_DEC_PINGPONG=1) DPRE / DO1 / their bias partials alternate between two slots branch by
-  // branch, so the model stream reuses a buffer only after the side's filter gradient of the
-  // branch before the previous one
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c2 = nullptr, ev_c1 = nullptr;
-  hipEvent_t ev_c2b = nullptr, ev_c1b = nullptr;
   float* bp_dec[2] = {nullptr, nullptr};
-  float* bp_dec2[2] = {nullptr, nullptr};
   bool pose_overlap() const { return pose_stream && side && !prof; }
   bool wgrad_overlap() const { return dec_wgrad_stream && side && !prof; }
   bool down_overlap() const { return down_stream && side && !prof; }
@@ -397,7 +384,7 @@ class Model {
     if (seg_ev) (void)hipEventDestroy(seg_ev);
     if (upd_ev) (void)hipEventDestroy(upd_ev);
     if (fork_ev) (void)hipEventDestroy(fork_ev);
-    for (hipEvent_t e : {ev_a, ev_b, ev_c2, ev_c1, ev_c2b, ev_c1b, ev_y[0], ev_y[1]})
+    for (hipEvent_t e : {ev_a, ev_b, ev_c2, ev_c1, ev_y[0], ev_y[1]})
       if (e) (void)hipEventDestroy(e);
     if (join_ev) (void)hipEventDestroy(join_ev);
     if (g.st) (void)hipStreamDestroy(g.st);
@@ -650,10 +637,6 @@ class Model {
     MD2_TRY(alloc(&DPRE, scratch));
     MD2_TRY(alloc(&DUP, scratch));
     MD2_TRY(alloc(&DO1, scratch));
-    if (dec_pingpong) {
-      MD2_TRY(alloc(&DPRE2, scratch));
-      MD2_TRY(alloc(&DO1b, scratch));
-    }
     {
       float* q;
       MD2_TRY(alloc(&q, wsn / sizeof(float) + 64));
@@ -675,12 +658,10 @@ class Model {
     MD2_HIP(hipEventCreateWithFlags(&upd_ev, hipEventDisableTiming));
     MD2_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     MD2_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
-    for (hipEvent_t* e : {&ev_a, &ev_b, &ev_c2, &ev_c1, &ev_c2b, &ev_c1b, &ev_y[0], &ev_y[1]})
+    for (hipEvent_t* e : {&ev_a, &ev_b, &ev_c2, &ev_c1, &ev_y[0], &ev_y[1]})
       MD2_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     MD2_TRY(alloc(&bp_dec[0], BP_WS));
     MD2_TRY(alloc(&bp_dec[1], BP_WS));
-    MD2_TRY(alloc(&bp_dec2[0], BP_WS));
-    MD2_TRY(alloc(&bp_dec2[1], BP_WS));
     {
       double* q;
       void* v;
@@ -1506,15 +1487,12 @@ class Model {
       DecBranch& d = br[i];
       const long hw = (long)d.h * d.w, hw2 = 4 * hw;
       const int co = d.b.cout;
-      // ping-pong slot of this branch (MD2_DEC_PINGPONG=0: one slot, A/B)
-      const int slot = dec_pingpong ? ((nb - 1 - i) & 1) : 0;
-      const int lag = dec_pingpong ? 2 : 1;
-      float* const dpre = slot ? DPRE2 : DPRE;
-      float* const do1 = slot ? DO1b : DO1;
-      const hipEvent_t evc2 = slot ? ev_c2b : ev_c2, evc1 = slot ? ev_c1b : ev_c1;
-      float* const bpc2 = slot ? bp_dec2[0] : bp_dec[0];
-      float* const bpc1 = slot ? bp_dec2[1] : bp_dec[1];
-      if (wov && i < nb - lag) MD2_HIP(hipStreamWaitEvent(st, evc2, 0));   // dpre, bpc2 free
+      float* const dpre = DPRE;
+      float* const do1 = DO1;
+      const hipEvent_t evc2 = ev_c2, evc1 = ev_c1;
+      float* const bpc2 = bp_dec[0];
+      float* const bpc1 = bp_dec[1];
+      if (wov && i < nb - 1) MD2_HIP(hipStreamWaitEvent(st, evc2, 0));   // dpre, bpc2 free
       MD2_TRY(act_bias(d.o2, d.d_o2, dpre, ND, co, hw2, ACT_ELU, st, wov ? bpc2 : nullptr));
       TensorIn in = tin(d.up, co, hw2);
       float* dskip = nullptr;
@@ -1533,7 +1511,7 @@ class Model {
           skip_bs = (long)featC[fi] * hw2;
         }
       }
-      if (wov && !((dec_wmain_c2 >> i) & 1)) {
+      if (wov) {
         MD2_TRY(wgrad_side(d.c2, in, dpre, ev_a, evc2));
         MD2_TRY(conv_d(d.c2, ND, dpre, DUP, co * hw2, 0, st, dskip, skip_bs, co));
       } else {
@@ -1544,7 +1522,7 @@ class Model {
         const int fi = 4 - d.b.bid;
         MD2_TRY(plane_sum(d_emb[fi], N, NP, featC[fi] + Ep, featC[fi], hw2, d_skip[fi], 0, st));
       }
-      if (wov && i < nb - lag) MD2_HIP(hipStreamWaitEvent(st, evc1, 0));   // do1, bpc1 free
+      if (wov && i < nb - 1) MD2_HIP(hipStreamWaitEvent(st, evc1, 0));   // do1, bpc1 free
       MD2_TRY(upsample2_bwd(DUP, ND, co, d.h, d.w, do1, st));
       MD2_TRY(act_bias(d.o1, do1, do1, ND, co, hw, ACT_ELU, st, wov ? bpc1 : nullptr));
       const float* xin;
@@ -1568,7 +1546,7 @@ class Model {
         dx = br[i - 1].d_o2;
         acc = br[i - 1].head >= 0 ? 1 : 0;   // on top of the head's dx
       }
-      if (wov && !((dec_wmain_c1 >> i) & 1)) {
+      if (wov) {
         MD2_TRY(wgrad_side(d.c1, tin(xin, cin, hw), do1, ev_b, evc1));
         MD2_TRY(conv_d(d.c1, ND, do1, dx, (long)cin * hw, acc, st));
       } else {
@@ -1578,7 +1556,7 @@ class Model {
         MD2_TRY(plane_sum(d_emb[4], N, NP, cin, featC[4], hw, d_f4 + (long)T0 * featC[4] * hw, 1, st));
     }
     // every decoder filter gradient final: the side runs in order, so its last event covers all
-    if (wov) MD2_HIP(hipStreamWaitEvent(st, (dec_pingpong && ((nb - 1) & 1)) ? ev_c1b : ev_c1, 0));
+    if (wov) MD2_HIP(hipStreamWaitEvent(st, ev_c1, 0));
     return MD2_OK;
   }
 

@@ -1116,6 +1116,8 @@ __global__ __launch_bounds__(256) void upsample2_bwd_kernel(const float* __restr
   float wy[6], wx[6];
   up_adj_weights(iy, ry, h, H2, oy0, wy);
   up_adj_weights(ix, rx, w, W2, ox0, wx);
+  // explicit fmas (the tiled kernel's order and roundings; a skipped zero weight is an exact
+  // fma(0, x, acc) = acc there)
   float s = 0.f;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
@@ -1124,8 +1126,8 @@ __global__ __launch_bounds__(256) void upsample2_bwd_kernel(const float* __restr
     float acc = 0.f;
 #pragma unroll
     for (int b = 0; b < 6; ++b)
-      if (wx[b] != 0.f) acc += wx[b] * row[ox0 + b];
-    s += wy[a] * acc;
+      if (wx[b] != 0.f) acc = fmaf(wx[b], row[ox0 + b], acc);
+    s = fmaf(wy[a], acc, s);
   }
   dx[i] = s;
 }
@@ -1308,15 +1310,17 @@ int concat_channels(const float* a, int ca, const float* b, int cb, int N, long 
 // equally stacked (N*C*2h) x 2w gradient, whatever plane they belong to -- an output row of a
 // neighbouring plane gets weight 0 from up_adj_weights (local index outside [0, 2h)), so a tile
 // may straddle planes and the small coarse levels (13 x 4 planes) fill whole blocks.  A block of
-// TW x TH input pixels stages its (2 TH + 4) x (2 TW + 4) output window in LDS with every
-// thread's loads issued before any LDS store (the one-at-a-time staging loop was latency-bound:
-// 39 us per launch), then contracts its 6 x 6 window from LDS with the same weights and the
-// same summation order as upsample2_bwd_kernel (bit-identical).
-template <int TW>
+// TW x (RPT * 256 / TW) input pixels stages its (2 TH + 4) x (2 TW + 4) output window in LDS with
+// every thread's loads issued before any LDS store, then each thread contracts RPT vertically
+// adjacent input pixels of one column (its six column weights computed once) from LDS with the
+// same weights and the same summation order as upsample2_bwd_kernel (bit-identical).  RPT = 4
+// (round 6): a quarter of the blocks, 4x the loads in flight per block and 4.5 instead of 5.3
+// staged floats per input pixel -- the one-row tiles were latency-bound (~1 TB/s).
+template <int TW, int RPT>
 __global__ __launch_bounds__(256) void upsample2_bwd_tile_kernel(const float* __restrict__ dy, int h,
                                                                  int w, long rows, float ry, float rx,
                                                                  float* __restrict__ dx) {
-  constexpr int TH = 256 / TW, FR = 2 * TH + 4, FC = 2 * TW + 4;
+  constexpr int TY = 256 / TW, TH = TY * RPT, FR = 2 * TH + 4, FC = 2 * TW + 4;
   constexpr int NL = (FR * FC + 255) / 256;
   __shared__ float t[FR][FC + 1];
   const int W2 = 2 * w;
@@ -1342,22 +1346,29 @@ __global__ __launch_bounds__(256) void upsample2_bwd_tile_kernel(const float* __
   __syncthreads();
   const int tx = threadIdx.x % TW, ty = threadIdx.x / TW;
   const int ix = ix0 + tx;
-  const long row = r0 + ty;
-  if (ix >= w || row >= rows) return;
-  const int iy = (int)(row % h);
-  int oy0, ox0;
-  float wy[6], wx[6];
-  up_adj_weights(iy, ry, h, 2 * h, oy0, wy);
+  if (ix >= w) return;
+  int ox0;
+  float wx[6];
   up_adj_weights(ix, rx, w, W2, ox0, wx);
-  float s = 0.f;
 #pragma unroll
-  for (int a = 0; a < 6; ++a) {
-    float acc = 0.f;
+  for (int k = 0; k < RPT; ++k) {
+    const int ly = ty * RPT + k;
+    const long row = r0 + ly;
+    if (row >= rows) break;
+    const int iy = (int)(row % h);
+    int oy0;
+    float wy[6];
+    up_adj_weights(iy, ry, h, 2 * h, oy0, wy);
+    float s = 0.f;
 #pragma unroll
-    for (int b = 0; b < 6; ++b) acc += wx[b] * t[2 * ty + a][2 * tx + b];
-    s += wy[a] * acc;
+    for (int a = 0; a < 6; ++a) {
+      float acc = 0.f;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) acc = fmaf(wx[b], t[2 * ly + a][2 * tx + b], acc);
+      s = fmaf(wy[a], acc, s);
+    }
+    dx[row * w + ix] = s;
   }
-  dx[row * w + ix] = s;
 }
 
 static inline float up_ratio(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
@@ -1376,12 +1387,12 @@ int upsample2_bwd(const float* dy, int N, int C, int h, int w, float* dx, hipStr
   MD2_TRY(check_u31(4 * n));
   static const int tiled = tuning_knob("MD2_UP_TILED", 1);
   const long rows = (long)N * C * h;
-  if (tiled && w > 16 && cdiv(rows, 8) <= 65535)
-    hipLaunchKernelGGL(upsample2_bwd_tile_kernel<32>, dim3(cdiv(w, 32), cdiv(rows, 8)), dim3(256), 0, st, dy, h,
-                       w, rows, up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx);
-  else if (tiled && cdiv(rows, 16) <= 65535)
-    hipLaunchKernelGGL(upsample2_bwd_tile_kernel<16>, dim3(cdiv(w, 16), cdiv(rows, 16)), dim3(256), 0, st, dy, h,
-                       w, rows, up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx);
+  if (tiled && w > 16 && cdiv(rows, 32) <= 65535)
+    hipLaunchKernelGGL((upsample2_bwd_tile_kernel<32, 4>), dim3(cdiv(w, 32), cdiv(rows, 32)), dim3(256), 0, st, dy,
+                       h, w, rows, up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx);
+  else if (tiled && cdiv(rows, 16) <= 65535)   // (4 rows per thread: 13.7 vs 10.3 us on the 4x13 maps)
+    hipLaunchKernelGGL((upsample2_bwd_tile_kernel<16, 1>), dim3(cdiv(w, 16), cdiv(rows, 16)), dim3(256), 0, st, dy,
+                       h, w, rows, up_ratio(h, 2 * h), up_ratio(w, 2 * w), dx);
   else
     hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dy, h, w,
                        up_ratio(h, 2 * h), up_ratio(w, 2 * w), fd(w), fd(h), dx, (uint32_t)n);

@@ -132,14 +132,15 @@ def test_tuning_knobs_ignored_without_md2_tuning(tmp_path):
 
 # round-5 placement / regrouping switches: each regroups the same arithmetic (other streams, other
 # buffers, another loop order with the same per-output fma chain), so the step must not move a bit
-BITWISE_TUNING = {"MD2_ENC_WGRAD_MAIN0": "0", "MD2_DEC_PINGPONG": "1", "MD2_HEAD_ROWS": "1"}
+BITWISE_TUNING = {"MD2_ENC_WGRAD_MAIN0": "0"}
 
 
 @pytest.mark.timeout(420)
 def test_bitwise_tuning_switches(tmp_path):
-    """MD2_ENC_WGRAD_MAIN0=0 (every layer-4 filter gradient on the side stream), MD2_DEC_PINGPONG=1
-    (two-slot decoder pullback buffers), MD2_HEAD_ROWS=1 (row-walking heads forward): two train
-    steps at B=2 64x128 give parameters bit-identical to the defaults."""
+    """MD2_ENC_WGRAD_MAIN0=0 (every layer-4 filter gradient on the side stream): two train steps at
+    B=2 64x128 give parameters bit-identical to the defaults.  (The round-5 opt-ins measured
+    neutral -- the decoder ping-pong buffers, the row-walking heads forward, the per-branch
+    decoder filter-gradient placement, the small-map whalo target -- were deleted in round 6.)"""
     import subprocess
     import sys
     import numpy as np

@@ -75,3 +75,36 @@ def test_upsample2(shape):
     (gx,) = torch.autograd.grad(yr, xr, dy.double())
     dx = ops.upsample2_backward(dy.to(DEV))
     assert D.rel_err(dx.cpu().double(), gx) < 1e-6
+
+
+_UP_CHILD = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/monodepth2.jl_amd"]
+from md2hip import ops
+out = []
+for shape in [(12, 16, 64, 208), (12, 32, 32, 104), (12, 256, 4, 13), (3, 4, 3, 7), (2, 3, 1, 1)]:
+    g = torch.Generator().manual_seed(5)
+    n, c, h, w = shape
+    dy = torch.randn(n, c, 2 * h, 2 * w, generator=g).cuda()
+    out.append(ops.upsample2_backward(dy).cpu().numpy().ravel())
+np.save(sys.argv[2], np.concatenate(out))
+"""
+
+
+def test_upsample2_backward_tiled_bit_identical_to_gather(tmp_path):
+    """The tiled adjoint (4 input rows per thread, round 6) equals the one-pixel-per-thread gather
+    kernel (MD2_UP_TILED=0) bit for bit at the decoder's shapes and odd ones."""
+    import os
+    import subprocess
+    import sys
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = {k: v for k, v in os.environ.items() if not k.startswith("MD2_")}
+    res = {}
+    for name, env in (("tiled", base), ("gather", dict(base, MD2_TUNING="1", MD2_UP_TILED="0"))):
+        out = str(tmp_path / f"{name}.npy")
+        r = subprocess.run([sys.executable, "-c", _UP_CHILD, root, out], env=env, capture_output=True,
+                           text=True, timeout=200)
+        assert r.returncode == 0, (name, r.stderr[-3000:])
+        res[name] = np.load(out)
+    assert np.array_equal(res["tiled"].view(np.uint32), res["gather"].view(np.uint32))
