@@ -15,7 +15,13 @@ pytestmark = pytest.mark.gpu
 
 # (x_shape, cout, k, stride, pad, reflect, act, bias)   -- shapes of the ResNet-18 / decoders
 CASES = [
-    ((2, 3, 64, 208), 64, 7, 2, 3, False, None, False),          # stem 7x7/2
+    ((2, 3, 64, 208), 64, 7, 2, 3, False, None, False),          # stem 7x7/2 (Wo = 104: conv_px)
+    # the stem on the space-to-depth kernel (conv_stem.inc, Wo % 16 == 0): two subtiles per row,
+    # a 2-row map (every s2d row window crosses a border) with an odd subtile count, 640 wide
+    # (8 staged records per thread, one block per CU)
+    ((3, 3, 32, 64), 64, 7, 2, 3, False, None, False),
+    ((2, 3, 4, 96), 64, 7, 2, 3, False, None, False),
+    ((1, 3, 10, 640), 64, 7, 2, 3, False, None, False),
     ((2, 64, 32, 104), 64, 3, 1, 1, False, None, False),         # layer1
     ((2, 64, 32, 104), 128, 3, 2, 1, False, None, False),        # layer2.0.conv1 (stride 2)
     ((2, 64, 32, 104), 128, 1, 2, 0, False, None, False),        # downsample 1x1/2

@@ -1,0 +1,27 @@
+#!/bin/bash
+# stem forward on the space-to-depth kernel: conv parity (stem cases), fusion / model parity,
+# per-kernel time (bench_conv under rocprof), step A/B against conv_px (MD2_STEM_S2D=0)
+set -o pipefail
+mkdir -p gpurun_out
+R=$GRAFT_REPO_ROOT
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_conv.py -k "k7" -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_r06l_conv.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_r06l_conv.log; [ $rc -eq 0 ] || { grep -E "^E " gpurun_out/pytest_r06l_conv.log | head -20; exit $rc; }
+cd /tmp && export TMPDIR=/tmp
+for v in 1 0; do
+  MD2_STEM_S2D=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_stem_$v -o run --output-format csv -- python3 $R/tools/bench_conv.py --only=stem > $R/gpurun_out/stem_$v.txt 2>&1 || exit 21
+  cat $R/gpurun_out/stem_$v.txt | grep stem
+  python3 - $R/gpurun_out/prof_stem_$v/run_kernel_stats.csv <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if any(k in r["Name"] for k in ("stem", "conv_px_kernel", "wgrad")):
+        print(f"  {r['Name'][:70]:70s} calls={r['Calls']} avg_us={float(r['AverageNs'])/1000:.1f}")
+PY
+done
+cd $R
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_fusion.py tests/test_gpu_model.py tests/test_gpu_forward_boundary.py -m gpu -q -x --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_r06l.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_r06l.log; [ $rc -eq 0 ] || { grep -E "^E " gpurun_out/pytest_r06l.log | head -20; exit $rc; }
+for rep in 1 2; do
+for v in 1 0; do
+  MD2_STEM_S2D=$v timeout -k 10 200 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/ab_r06l.json 2>/dev/null || exit 23
+  python3 -c "import json,sys; d=json.load(open('gpurun_out/ab_r06l.json')); print('MD2_STEM_S2D=%s %9.1f img/s  %.3f ms' % (sys.argv[1], d['value'], d['ms_per_step']))" "$v"
+done; done
