@@ -57,12 +57,9 @@ struct SplitKDefer {
   // BatchNorm statistics from the conv epilogue (conv_fwd only): the caller offers a partials
   // buffer [Cout][>= ceil(N*Ho*Wo / 256)][2] (fp64 sum, sum of squares); when the conv runs the
   // LDS-halo kernel without split-K it writes one partial per 256-pixel tile and sets
-  // stats_parts to the tile count (0: not written, run bn_stats_partial as usual); the stem
-  // kernel (conv_stem.inc) writes two per block (stats_collapse): conv_fwd_stats_parts
+  // stats_parts to the tile count (0: not written, run bn_stats_partial as usual)
   double* stats = nullptr;
   int stats_parts = 0;
-  bool stats_collapse = false;   // output: the partials are few per block but many per channel --
-                                 // collapse them before the apply passes finalise per block
   bool keep_reduce = false;   // input: never defer the split-K reduction (only the statistics)
 };
 
@@ -84,8 +81,6 @@ bool conv_px16_used(const ConvShape& s, int mode);   // M <= 16 (16x16x4 MFMA ke
 
 // packed operand sizes (elements) -- weights are repacked K-major with zero padding
 size_t conv_fwd_packed_elems(const ConvShape& s);
-// most BN-statistics partials per channel conv_fwd's epilogue writes for this shape (SplitKDefer)
-long conv_fwd_stats_parts(const ConvShape& s);
 size_t conv_dgrad_packed_elems(const ConvShape& s);
 int conv_pack_fwd(const ConvShape& s, const float* w, float* packed, hipStream_t st);
 int conv_pack_dgrad(const ConvShape& s, const float* w, float* packed, hipStream_t st);

@@ -478,11 +478,6 @@ class Model {
     // ---- encoder
     MD2_TRY(make_conv(stem, spec.stem, cfg.H, cfg.W, false, wsn));
     need_ws(stem, B, wsn, false);
-    {
-      ConvShape ss = stem.s;
-      ss.N = B;
-      bnmax = std::max(bnmax, (long)ss.Cout * conv_fwd_stats_parts(ss) * 2);   // the stem's per-row partials
-    }
     MD2_TRY(make_bn(stem_bn, spec.stem_bn));
     H0 = stem.s.Ho;
     W0 = stem.s.Wo;
@@ -806,7 +801,7 @@ class Model {
     if (d.stats_parts > 0) {
       // (the apply passes finalise the tile partials per block, behind their own loads;
       // MD2_BN_COLLAPSE=1: one collapse launch first -- measured slower, 6 us per launch)
-      if (bn_collapse || d.stats_collapse) {
+      if (bn_collapse) {
         MD2_CHECK_ARG(bn.p.c <= 4096, "conv_f_bn: BN channels");
         double* col = bn_collapsed + (long)slot * 2 * 4096;
         MD2_TRY(bn_partials_collapse(wst.partials, bn.p.c, d.stats_parts, col, st));
