@@ -112,6 +112,10 @@ size_t conv_fwd_workspace(const ConvShape& s);
 size_t conv_dgrad_workspace(const ConvShape& s);
 size_t conv_wgrad_workspace(const ConvShape& s);
 
+// arithmetic of the last conv kernel launched by this host thread (profiling labels): 6 = bf16x6
+// split products on the bf16 MFMA (issued ceiling 2516 / 6 TFLOP/s fp32-equivalent), 1 = fp32
+// MFMA, 0 = VALU (the Cout = 1 heads)
+int conv_last_arith();
 int conv_fwd(const ConvShape& s, const TensorIn& x, const float* wpacked, const TensorOut& y,
              ConvWorkspace ws, hipStream_t st, SplitKDefer* defer = nullptr);
 // dX from dY (dY: [N][Cout][Ho][Wo] pre-activation gradient)

@@ -752,9 +752,12 @@ class Model {
     hipEvent_t b = ev();
     (void)hipEventRecord(b, st);
     ProfRec r{a, b, cat, work, {0}};
-    if (pass && s)
-      snprintf(r.tag, sizeof(r.tag), "%s %dx%d/%d%s %d->%d %dx%d n%d", pass, s->KH, s->KW, s->stride,
-               s->reflect ? "r" : "", s->Cin, s->Cout, s->H, s->W, s->N);
+    if (pass && s) {
+      const int ar = conv_last_arith();
+      snprintf(r.tag, sizeof(r.tag), "%s %dx%d/%d%s %d->%d %dx%d n%d [%s]", pass, s->KH, s->KW, s->stride,
+               s->reflect ? "r" : "", s->Cin, s->Cout, s->H, s->W, s->N,
+               ar == 6 ? "bf16x6" : ar == 1 ? "fp32" : "valu");
+    }
     else if (pass)
       snprintf(r.tag, sizeof(r.tag), "%s", pass);
     recs.push_back(r);
