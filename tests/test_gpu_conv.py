@@ -203,9 +203,12 @@ from md2hip import ops
 from oracle import md2_oracle as O
 from tests import _data as D
 out = {}
-for xs, cout, k, st, pd, rf in [((36, 64, 32, 104), 64, 3, 1, 1, False), ((36, 128, 16, 52), 256, 3, 2, 1, False),
-                                ((36, 512, 4, 13), 512, 3, 1, 1, False), ((12, 128, 32, 104), 64, 3, 1, 1, True),
-                                ((36, 128, 16, 52), 256, 1, 2, 0, False)]:
+shapes = [((36, 64, 32, 104), 64, 3, 1, 1, False), ((36, 128, 16, 52), 256, 3, 2, 1, False),
+          ((36, 512, 4, 13), 512, 3, 1, 1, False), ((12, 128, 32, 104), 64, 3, 1, 1, True),
+          ((36, 128, 16, 52), 256, 1, 2, 0, False)]
+if len(sys.argv) > 2:
+    shapes = [(tuple(a), b, c, d, e, f) for a, b, c, d, e, f in json.loads(sys.argv[2])]
+for xs, cout, k, st, pd, rf in shapes:
     g = torch.Generator().manual_seed(5)
     x = torch.randn(*xs, generator=g, dtype=torch.float64).float().double()
     w = (torch.randn(cout, xs[1], k, k, generator=g, dtype=torch.float64) / (xs[1] * k * k) ** 0.5).float().double()
@@ -226,6 +229,18 @@ print(json.dumps(out))
 @pytest.mark.parametrize("env", [{"MD2_PX3": "0", "MD2_WPX3": "0"}, {"MD2_PX3_TERMS": "9"}],
                          ids=["fp32-mfma", "bf16x9"])
 def test_conv_kernel_variants(env):
+    _variant(env)
+
+
+def test_halo2d_dgrad_variant():
+    """The 2D-tile halo kernel's data-gradient forms (MD2_HALO2D=3: off by default, measured
+    slower in the step): the reflect dgrad on the padded grid + fold at the decoder's 96->32
+    64x208 shape and a ragged one, the zero-padded dgrad with 32-row M tiles; within 1e-5 of fp64."""
+    _variant({"MD2_HALO2D": "3"}, [[[12, 96, 64, 208], 32, 3, 1, 1, True], [[3, 96, 20, 70], 32, 3, 1, 1, True],
+                                   [[2, 32, 24, 200], 64, 3, 1, 1, False], [[2, 96, 16, 60], 48, 3, 1, 1, False]])
+
+
+def _variant(env, shapes=None):
     """The selectable conv kernels (MD2_TUNING=1): the exact-fp32 MFMA kernels (conv_px2 for
     fwd / dgrad, conv_wgrad_tap for wgrad) and the nine-product bf16x9 form of conv_px3 /
     conv_wgrad_px3, on encoder / decoder shapes, within
@@ -236,8 +251,8 @@ def test_conv_kernel_variants(env):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     e = {k: v for k, v in os.environ.items() if not k.startswith("MD2_")}
     e.update(MD2_TUNING="1", **env)
-    r = subprocess.run([sys.executable, "-c", _VARIANT_CHILD, root], env=e, capture_output=True, text=True,
-                       timeout=240)
+    argv = [sys.executable, "-c", _VARIANT_CHILD, root] + ([json.dumps(shapes)] if shapes else [])
+    r = subprocess.run(argv, env=e, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     errs = json.loads(r.stdout.strip().splitlines()[-1])
     bad = {k: v for k, v in errs.items() if max(v) >= 1e-5}
