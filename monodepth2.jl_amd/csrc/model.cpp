@@ -327,7 +327,7 @@ class Model {
   bool pose_overlap() const { return pose_stream && side && !prof; }
   bool wgrad_overlap() const { return dec_wgrad_stream && side && !prof; }
   bool down_overlap() const { return down_stream && side && !prof; }
-  // Encoder backward of the last stage (stages >= enc_wgrad_from: layer 4 by default; its convs
+  // Encoder backward of the last stages (stages >= enc_wgrad_from: layers 2-4 by default; the convs
   // are small and split-K): each block conv's filter gradient on the side stream beside its data
   // gradient (interleaved A/B, 3 x 60 steps: off 1481, from layer 4 1493, from layer 3 1490,
   // from layer 2 1478 images/s -- the larger layers' convs fill the chip and only time-share).  The
@@ -338,7 +338,9 @@ class Model {
     const char* v = getenv("MD2_ENC_WGRAD_STREAM");
     return !(v && v[0] == '0');
   }();
-  const int enc_wgrad_from = tuning_knob("MD2_ENC_WGRAD_FROM", 3);
+  // (round 6, with the LDS-halo kernels: from layer 2 (si = 1) 6.194 vs 6.211 ms and 6.159 vs 6.19
+  // against layer 4 only, interleaved; from layer 1 6.167)
+  const int enc_wgrad_from = tuning_knob("MD2_ENC_WGRAD_FROM", 1);
   // (1: -45 us per step, 6.555 vs 6.60 ms interleaved; the side stream was the longer path of the
   // layer-4 segment)
   const bool enc_wgrad_main0 = tuning_knob("MD2_ENC_WGRAD_MAIN0", 1) != 0;
