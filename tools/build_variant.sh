@@ -7,7 +7,7 @@ NAME=$1; UNIT=$2; FLAGS=${3:-}
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/monodepth2.jl_amd/csrc
 make -C "$C" -j16 > /dev/null
-OUT=$R/lib_var/$NAME
+OUT=${VAR_DIR:-$R/lib_var}/$NAME
 mkdir -p "$OUT"
 base=$(basename "$UNIT" .hip)
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 $FLAGS \
