@@ -9,7 +9,7 @@ C=$R/monodepth2.jl_amd/csrc
 make -C "$C" -j16 > /dev/null
 OUT=${VAR_DIR:-$R/lib_var}/$NAME
 mkdir -p "$OUT"
-base=$(basename "$UNIT" .hip)
+base=$(basename "${UNIT%.*}")
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 $FLAGS \
   -c "$C/$UNIT" -o "$OUT/$base.o"
 objs=$(ls "$C"/build/*.o | grep -v "/$base.o$")
