@@ -105,6 +105,16 @@ CASES = [
     # then the fold): many small padded images per tile, a 2-row map (every row folds)
     ((3, 64, 7, 5), 64, 3, 1, 1, True, "elu", True),
     ((4, 128, 2, 9), 64, 3, 1, 1, True, None, False),
+    # stride-2 data gradient on the LDS halo (conv_halo3s2: the four output-parity classes from
+    # one staged dY image): 128-point tiles over many 3x7 images, a 1x1 dY map, 64- and 65-wide dY
+    # rows (the widest its 416-pixel halo plane takes), a 100-wide one (too wide: conv_px3's merged
+    # classes), Cout 64 (4 chunks, split-K of 2)
+    ((5, 64, 6, 14), 64, 3, 2, 1, False, None, False),
+    ((2, 64, 2, 2), 64, 3, 2, 1, False, None, False),
+    ((2, 64, 4, 128), 64, 3, 2, 1, False, None, False),
+    ((1, 128, 6, 130), 64, 3, 2, 1, False, "relu", True),
+    ((2, 64, 4, 200), 64, 3, 2, 1, False, None, False),
+    ((3, 192, 10, 30), 64, 3, 2, 1, False, None, False),
     # every conv of the benchmarked step (BASELINE config 3: B=12 triplets, 416x128) at its bench
     # shape -- the encoder on 36 frames, the pose decoder on 24 pairs, the depth decoder on the 12
     # targets -- so each planner choice the bench runs (tile, split-K count, stride-2 phase launch,
@@ -238,6 +248,13 @@ def test_halo2d_dgrad_variant():
     64x208 shape and a ragged one, the zero-padded dgrad with 32-row M tiles; within 1e-5 of fp64."""
     _variant({"MD2_HALO2D": "3"}, [[[12, 96, 64, 208], 32, 3, 1, 1, True], [[3, 96, 20, 70], 32, 3, 1, 1, True],
                                    [[2, 32, 24, 200], 64, 3, 1, 1, False], [[2, 96, 16, 60], 48, 3, 1, 1, False]])
+
+
+def test_halo_s2_off_variant():
+    """MD2_HALO_S2=0: the stride-2 data gradients back on conv_px3's merged parity classes (the
+    path the halo kernel replaced), at the encoder's three bench shapes; within 1e-5 of fp64."""
+    _variant({"MD2_HALO_S2": "0"}, [[[36, 64, 32, 104], 128, 3, 2, 1, False], [[36, 128, 16, 52], 256, 3, 2, 1, False],
+                                    [[36, 256, 8, 26], 512, 3, 2, 1, False]])
 
 
 def _variant(env, shapes=None):

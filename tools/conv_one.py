@@ -7,7 +7,9 @@ from md2hip import ops
 from md2hip._lib import lib, ptr, stream_of, check
 SHAPES = {"l2": ((36, 128, 16, 52), 128, 3, 1, 1, 0), "l1": ((36, 64, 32, 104), 64, 3, 1, 1, 0),
           "l3": ((36, 256, 8, 26), 256, 3, 1, 1, 0), "l4": ((36, 512, 4, 13), 512, 3, 1, 1, 0), "d4": ((12, 96, 64, 208), 32, 3, 1, 1, 1),
-          "stem": ((36, 3, 128, 416), 64, 7, 2, 3, 0)}
+          "stem": ((36, 3, 128, 416), 64, 7, 2, 3, 0),
+          "s2l2": ((36, 64, 32, 104), 128, 3, 2, 1, 0), "s2l3": ((36, 128, 16, 52), 256, 3, 2, 1, 0),
+          "s2l4": ((36, 256, 8, 26), 512, 3, 2, 1, 0)}
 xs, cout, k, st, pd, rf = SHAPES[sys.argv[1] if len(sys.argv) > 1 else "l2"]
 only = sys.argv[2] if len(sys.argv) > 2 else "all"
 x = torch.randn(*xs, device="cuda")

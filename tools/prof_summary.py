@@ -39,6 +39,8 @@ def is_conv3(name):
         return False
     if "conv_halo3_kernel" in name:        # <MODE, NT, ITEMS, DBG, RFL, EXT>: stride-1 3x3
         return (len(a) < 5 or a[4] == 0) and (len(a) < 6 or a[5] == 0)
+    if "conv_halo3s2_kernel" in name:      # <ITEMS>: stride-2 3x3 data gradient
+        return True
     if "conv_whalo_kernel" in name:        # <ITEMS, KS>: stride-1 3x3 zero-padded filter gradient
         return True
     if "conv_wgrad_px3_kernel" in name:    # <BM, BN, WM, WN, KH, KW, S, RFL, CW, NT>
@@ -89,6 +91,8 @@ def conv3_family(name):
     if not is_conv3(name):
         return None
     a = targs(name)
+    if "conv_halo3s2_kernel" in name:
+        return "dgrad halo3s2 (stride 2)"
     if "conv_halo3_kernel" in name:
         return ("fwd" if a[0] == 0 else "dgrad") + " halo3"
     if "conv_whalo_kernel" in name:
